@@ -1,0 +1,7 @@
+"""Put the repository root on sys.path so the shims below can import the package."""
+import os
+import sys
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if _ROOT not in sys.path:
+    sys.path.insert(0, _ROOT)

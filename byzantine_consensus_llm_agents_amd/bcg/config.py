@@ -1,0 +1,96 @@
+"""Configuration registry for the Byzantine Consensus Game (BCG).
+
+Same module-level dict schema as the reference (``bcg/config.py:7-77``): the
+dicts are plain mutable objects and are mutated at runtime by the CLI
+(``main.main``) and by ``run_simulation`` exactly like the reference does
+(``bcg/main.py:1042``, ``:1097-1102``).  Everything specific to the MI355X
+engine lives in ``ENGINE_CONFIG`` (new), so code written against the
+reference's config keeps working unchanged.
+"""
+
+import os
+
+# --- communication / network (reference bcg/config.py:7-15) -----------------
+COMMUNICATION_CONFIG = {
+    "protocol_type": "a2a_sim",
+}
+
+NETWORK_CONFIG = {
+    "topology_type": "fully_connected",  # fully_connected | ring | grid | custom
+    "custom_adjacency": None,
+}
+
+# --- model presets (reference bcg/config.py:20-25) + the plumbing model ------
+MODEL_PRESETS = {
+    "qwen3-8b": "Qwen/Qwen3-8B",
+    "qwen3-14b": "Qwen/Qwen3-14B",
+    "qwen3-32b": "Qwen/Qwen3-32B",
+    "mistral-22b": "mistralai/Mistral-Small-Instruct-2409",
+    "qwen2.5-0.5b": "Qwen/Qwen2.5-0.5B-Instruct",
+}
+
+ACTIVE_MODEL = "qwen3-14b"
+
+# Engine knobs keep the reference's key names (bcg/config.py:33-41).  On the
+# MI355X engine `max_num_seqs` is only honoured in reference-emulation mode
+# (ENGINE_CONFIG["honor_max_num_seqs"]); `quantization` selects the fp8 path.
+VLLM_CONFIG = {
+    "model_name": MODEL_PRESETS[ACTIVE_MODEL],
+    "max_model_len": 8192,
+    "gpu_memory_utilization": 0.9,
+    "tensor_parallel_size": 1,
+    "max_num_seqs": 4,
+    "quantization": None,
+    "disable_qwen3_thinking": True,
+}
+
+AGENT_CONFIG = {
+    "use_structured_output": True,
+    "use_batched_inference": True,
+}
+
+# Single source of truth for sampling (reference bcg/config.py:52-58).
+LLM_CONFIG = {
+    "temperature_decide": 0.5,
+    "temperature_vote": 0.3,
+    "max_tokens_decide": 300,
+    "max_tokens_vote": 200,
+    "max_json_retries": 3,
+}
+
+BCG_CONFIG = {
+    "num_honest": 8,
+    "num_byzantine": 0,
+    "value_range": (0, 50),
+    "consensus_threshold": 66.0,
+    "max_rounds": 50,
+}
+
+METRICS_CONFIG = {
+    "track_convergence": True,
+    "track_byzantine_impact": True,
+    "track_communication": True,
+    "save_results": True,
+    "generate_plots": False,
+    "results_dir": "results",
+}
+
+# --- MI355X engine (new) -----------------------------------------------------
+# backend: "hip"  -> in-process MI355X engine (HIP kernels, RCCL for TP)
+#          "torch"-> same engine on torch reference ops (CPU / debugging)
+#          "fake" -> scripted schema-valid responses, no model (plumbing/tests)
+ENGINE_CONFIG = {
+    "backend": os.environ.get("BCG_ENGINE", "auto"),
+    "weights": os.environ.get("BCG_WEIGHTS", "auto"),  # auto | random | <dir with safetensors>
+    "dtype": "bfloat16",
+    "kv_block_size": 16,
+    "seed": None,                  # None = unseeded (reference behaviour)
+    "budget_aware_json": False,    # force closing JSON before max_tokens
+    "max_whitespace": 4,           # JSON grammar: max consecutive whitespace chars
+    "prefix_caching": True,
+    "use_hip_graphs": True,
+    "max_batch_seqs": 512,
+    "prefill_chunk_tokens": 16384,
+    "honor_max_num_seqs": False,
+    "kv_cache_gb": None,           # None = size from gpu_memory_utilization
+}

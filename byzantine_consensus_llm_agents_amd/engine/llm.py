@@ -1,0 +1,204 @@
+"""User-facing engine API (the L0 boundary the reference reached through vLLM).
+
+``LLM.generate(prompts, sampling_params)`` mirrors the vLLM call sites used by
+the reference (``bcg/vllm_agent.py:144, :331, :430``) with one extension that
+removes the reference's batch-size-1 fallback: ``sampling_params`` may be a
+*list*, one per prompt, each with its own ``GuidedDecodingParams(json=...)``.
+
+Backends:
+  * ``hip``   - :class:`..engine.engine.InferenceEngine` with the HIP kernels
+                (MI355X); fails loudly if the kernel library is missing;
+  * ``torch`` - the same engine on PyTorch reference ops (CPU tests);
+  * ``fake``  - scripted schema-valid answers (plumbing, parity tests).
+
+Several simulations may share one ``LLM`` from different threads: calls are
+coalesced (:class:`Coalescer`) into a single device batch once every
+registered simulation is waiting on the engine, which is how one GPU serves
+many independent BCG seeds per batched round.
+"""
+
+import os
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence, Union
+
+from ..bcg.config import ENGINE_CONFIG
+
+
+@dataclass
+class GuidedDecodingParams:
+    json: Optional[Dict[str, Any]] = None
+
+
+@dataclass
+class SamplingParams:
+    temperature: float = 1.0
+    top_p: float = 1.0
+    max_tokens: int = 16
+    guided_decoding: Optional[GuidedDecodingParams] = None
+    seed: Optional[int] = None
+
+
+@dataclass
+class CompletionOutput:
+    index: int
+    text: str
+    token_ids: List[int] = field(default_factory=list)
+    finish_reason: str = "stop"
+
+
+@dataclass
+class RequestOutput:
+    request_id: int
+    prompt: str
+    outputs: List[CompletionOutput]
+    num_prompt_tokens: int = 0
+    num_cached_tokens: int = 0
+
+
+class Coalescer:
+    """Merge concurrent ``generate`` calls from registered threads into one batch."""
+
+    def __init__(self, run_batch):
+        self._run = run_batch
+        self._cond = threading.Condition()
+        self._participants = 0
+        self._tickets: List[dict] = []
+
+    def join(self):
+        with self._cond:
+            self._participants += 1
+
+    def leave(self):
+        with self._cond:
+            self._participants -= 1
+            self._maybe_flush_locked()
+
+    def _maybe_flush_locked(self):
+        waiting = [t for t in self._tickets if not t["done"]]
+        if waiting and len(waiting) >= self._participants:
+            self._tickets = []
+            self._cond.release()
+            try:
+                self._flush(waiting)
+            finally:
+                self._cond.acquire()
+            self._cond.notify_all()
+
+    def _flush(self, tickets):
+        prompts, params, spans = [], [], []
+        for t in tickets:
+            spans.append((len(prompts), len(t["prompts"])))
+            prompts += t["prompts"]
+            params += t["params"]
+        try:
+            texts = self._run(prompts, params)
+            for t, (a, n) in zip(tickets, spans):
+                t["result"] = texts[a:a + n]
+        except Exception as exc:  # every caller sees the engine failure
+            for t in tickets:
+                t["error"] = exc
+        for t in tickets:
+            t["done"] = True
+
+    def submit(self, prompts, params):
+        ticket = {"prompts": prompts, "params": params, "done": False}
+        with self._cond:
+            self._tickets.append(ticket)
+            self._maybe_flush_locked()
+            while not ticket["done"]:
+                self._cond.wait()
+        if "error" in ticket:
+            raise ticket["error"]
+        return ticket["result"]
+
+
+def resolve_backend(requested: Optional[str]) -> str:
+    name = (requested or ENGINE_CONFIG.get("backend") or "auto").lower()
+    if name != "auto":
+        return name
+    try:
+        import torch
+        if torch.cuda.device_count() > 0:
+            return "hip"
+    except Exception:
+        pass
+    return "fake"
+
+
+class LLM:
+    """In-process engine facade (one per process / TP group)."""
+
+    def __init__(self, model: str, max_model_len: int = 8192, gpu_memory_utilization: float = 0.9,
+                 tensor_parallel_size: int = 1, max_num_seqs: Optional[int] = None,
+                 quantization: Optional[str] = None, backend: Optional[str] = None,
+                 weights: Optional[str] = None, seed: Optional[int] = None, **kwargs):
+        self.model = model
+        self.backend_name = resolve_backend(backend)
+        seed = seed if seed is not None else ENGINE_CONFIG.get("seed")
+        if self.backend_name == "fake":
+            from .fake import FakeBackend
+            self.backend = FakeBackend(seed=seed or 0)
+        elif self.backend_name in ("hip", "torch"):
+            from .engine import EngineArgs, InferenceEngine
+            args = EngineArgs.from_configs(model, max_model_len=max_model_len,
+                                           gpu_memory_utilization=gpu_memory_utilization,
+                                           tensor_parallel_size=tensor_parallel_size,
+                                           max_num_seqs=max_num_seqs, quantization=quantization,
+                                           backend=self.backend_name, weights=weights, seed=seed,
+                                           **kwargs)
+            self.backend = InferenceEngine(args)
+        else:
+            raise ValueError(f"unknown engine backend {self.backend_name!r}")
+        self.coalescer = Coalescer(self._run_batch)
+        self._coalesce = False
+        self._next_id = 0
+        self.stats = {"calls": 0, "sequences": 0, "seconds": 0.0}
+
+    # --------------------------------------------------- multi-sim sharing
+    def register_client(self):
+        """Declare one more simulation thread whose calls should be coalesced."""
+        self._coalesce = True
+        self.coalescer.join()
+
+    def unregister_client(self):
+        self.coalescer.leave()
+
+    # ------------------------------------------------------------- serving
+    def _run_batch(self, prompts: List[str], params: List[SamplingParams]) -> List[str]:
+        t0 = time.perf_counter()
+        texts = self.backend.generate(prompts, params)
+        self.stats["calls"] += 1
+        self.stats["sequences"] += len(prompts)
+        self.stats["seconds"] += time.perf_counter() - t0
+        return texts
+
+    def generate(self, prompts: Union[str, Sequence[str]],
+                 sampling_params: Union[SamplingParams, Sequence[SamplingParams], None] = None,
+                 use_tqdm: bool = False) -> List[RequestOutput]:
+        if isinstance(prompts, str):
+            prompts = [prompts]
+        prompts = list(prompts)
+        if sampling_params is None:
+            sampling_params = SamplingParams()
+        if isinstance(sampling_params, SamplingParams):
+            params = [sampling_params] * len(prompts)
+        else:
+            params = list(sampling_params)
+            if len(params) != len(prompts):
+                raise ValueError("need one SamplingParams per prompt")
+        if not prompts:
+            return []
+        if self._coalesce:
+            texts = self.coalescer.submit(prompts, params)
+        else:
+            texts = self._run_batch(prompts, params)
+        outs = []
+        for p, t in zip(prompts, texts):
+            outs.append(RequestOutput(self._next_id, p, [CompletionOutput(0, t)]))
+            self._next_id += 1
+        return outs
+
+    def shutdown(self):
+        self.backend.shutdown()

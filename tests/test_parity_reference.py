@@ -1,0 +1,69 @@
+"""Simulator parity against golden runs of the reference (tools/gen_golden.py).
+
+The reference and this framework are driven by the same scripted engine
+(engine/fake.py) and the same global ``random`` seed; the exact prompts sent to
+the engine (flattened in order), the results JSON (minus timestamps) and the
+CSV header must be identical.  Engine-call *counts* differ on purpose: the
+reference falls back to one call per prompt when schemas differ, we never do.
+"""
+import glob
+import json
+import os
+import random
+
+import pytest
+
+from byzantine_consensus_llm_agents_amd.engine import fake as fake_mod
+
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "ref_*.json")))
+
+
+def _run_ours(rec, tmp_path, cfg, monkeypatch):
+    from byzantine_consensus_llm_agents_amd.bcg.simulation import BCGSimulation
+    sent = []
+    orig = fake_mod.FakeBackend.generate
+
+    def recording(self, prompts, params):
+        for p, sp in zip(prompts, params):
+            sent.append((p, sp.guided_decoding.json if sp.guided_decoding else None,
+                         sp.temperature, sp.max_tokens))
+        return orig(self, prompts, params)
+
+    monkeypatch.setattr(fake_mod.FakeBackend, "generate", recording)
+    monkeypatch.chdir(tmp_path)
+    cfg.ENGINE_CONFIG["backend"] = "fake"
+    cfg.BCG_CONFIG["value_range"] = tuple(rec["value_range"])
+    random.seed(rec["seed"])
+    sim = BCGSimulation(num_honest=rec["honest"], num_byzantine=rec["byzantine"], config={
+        "max_rounds": rec["rounds"], "consensus_threshold": 66.0,
+        "value_range": tuple(rec["value_range"]), "verbose": False,
+        "byzantine_awareness": rec["awareness"]})
+    sim.run()
+    with open(os.path.join(tmp_path, "results", "json", "run_001.json")) as fh:
+        results = json.load(fh)
+    with open(os.path.join(tmp_path, "results", "metrics", "run_001.csv")) as fh:
+        header = fh.read().splitlines()[0]
+    return sent, results, header
+
+
+@pytest.mark.skipif(not GOLDEN, reason="no golden fixtures")
+@pytest.mark.parametrize("path", GOLDEN, ids=lambda p: os.path.basename(p)[4:-5])
+def test_reference_parity(path, tmp_path, fresh_engine_state, monkeypatch):
+    with open(path) as fh:
+        rec = json.load(fh)
+    sent, results, header = _run_ours(rec, tmp_path, fresh_engine_state, monkeypatch)
+
+    ref_prompts = [(p, s, c["temperature"], c["max_tokens"])
+                   for c in rec["engine_calls"] for p, s in zip(c["prompts"], c["schemas"])]
+    assert len(sent) == len(ref_prompts)
+    for i, (ours, ref) in enumerate(zip(sent, ref_prompts)):
+        assert ours[0] == ref[0], f"prompt {i} differs"
+        assert ours[1] == ref[1], f"schema {i} differs"
+        assert ours[2:] == tuple(ref[2:]), f"sampling params {i} differ"
+
+    results.pop("timestamp", None)
+    results["metrics"].pop("timestamp", None)
+    assert results == rec["results"]
+    assert header == rec["csv_header"]
+    # one engine call per phase attempt on our side, never per prompt
+    assert len(rec["engine_calls"]) >= sum(1 for _ in rec["engine_calls"] if _["n"] > 1)
