@@ -1,0 +1,135 @@
+"""Schema -> token-level FSM tables, cached and packed into one device tensor.
+
+``FSMRegistry.get(schema)`` returns the row base of the schema's table inside
+a single ``int16 [rows, vocab]`` device tensor (``table``) plus a per-row
+``dist`` vector.  A decoding sequence carries ``(fsm_base, fsm_state)``; the
+sampling kernel reads ``table[fsm_base + fsm_state]`` -- so any mix of
+schemas shares one batch (the fix for the reference's batch-size-1
+fallback).
+"""
+
+import hashlib
+import json
+import threading
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .json_schema import schema_to_dfa
+
+
+@dataclass
+class CompiledFSM:
+    key: str
+    next: np.ndarray     # int16 [S, V]
+    dist: np.ndarray     # int16 [S]
+    num_byte_states: int
+
+    @property
+    def num_states(self) -> int:
+        return self.next.shape[0]
+
+
+def compile_schema(schema: Dict, token_bytes: List[bytes], vocab_rows: int, max_ws: int = 4,
+                   native: bool = True) -> CompiledFSM:
+    dfa = schema_to_dfa(schema, max_ws=max_ws)
+    key = json.dumps(schema, sort_keys=True)
+    if native:
+        from ...runtime import compile_token_fsm
+        nxt, dist = compile_token_fsm(dfa.trans, dfa.accept.astype(np.uint8), token_bytes, vocab_rows)
+    else:
+        nxt, dist = compile_token_fsm_py(dfa.trans, dfa.accept, token_bytes, vocab_rows)
+    return CompiledFSM(key, np.asarray(nxt), np.asarray(dist), dfa.num_states)
+
+
+def compile_token_fsm_py(trans: np.ndarray, accept: np.ndarray, token_bytes: List[bytes], vocab_rows: int):
+    """Pure-Python oracle of csrc/runtime/token_fsm.cpp (small vocabularies only)."""
+    S = trans.shape[0]
+    nxt = np.full((S, vocab_rows), -1, dtype=np.int16)
+    for s in range(S):
+        for t, tb in enumerate(token_bytes[:vocab_rows]):
+            if not tb:
+                continue
+            cur = s
+            for b in tb:
+                cur = int(trans[cur, b])
+                if cur < 0:
+                    break
+            if cur >= 0:
+                nxt[s, t] = cur
+    dist = np.full(S, np.iinfo(np.int16).max, dtype=np.int16)
+    dist[accept.astype(bool)] = 0
+    changed = True
+    while changed:
+        changed = False
+        for s in range(S):
+            row = nxt[s]
+            valid = row[row >= 0]
+            if valid.size:
+                best = int(dist[valid].min())
+                if best < np.iinfo(np.int16).max and best + 1 < dist[s]:
+                    dist[s] = best + 1
+                    changed = True
+    return nxt, dist
+
+
+class FSMRegistry:
+    """Compiles schemas on first use and keeps all tables resident on the device."""
+
+    def __init__(self, token_bytes: List[bytes], vocab_rows: int, device, max_ws: int = 4,
+                 native: bool = True):
+        self.token_bytes = token_bytes
+        self.vocab_rows = vocab_rows
+        self.device = torch.device(device)
+        self.max_ws = max_ws
+        self.native = native
+        self._lock = threading.Lock()
+        self._bases: Dict[str, int] = {}
+        self._fsms: Dict[str, CompiledFSM] = {}
+        self.capacity = 0
+        self.table = torch.full((1, vocab_rows), -1, dtype=torch.int16, device=self.device)
+        self.dist = torch.full((1,), 0, dtype=torch.int16, device=self.device)
+        self.rows = 0
+        self.version = 0  # bumped whenever `table`/`dist` are re-allocated (graphs must re-capture)
+
+    @staticmethod
+    def key_of(schema: Dict) -> str:
+        return json.dumps(schema, sort_keys=True)
+
+    def get(self, schema: Dict) -> int:
+        key = self.key_of(schema)
+        with self._lock:
+            base = self._bases.get(key)
+            if base is not None:
+                return base
+            fsm = compile_schema(schema, self.token_bytes, self.vocab_rows, self.max_ws, self.native)
+            base = self.rows
+            new_rows = self.rows + fsm.num_states
+            if new_rows > self.capacity:
+                # geometric growth keeps re-allocations (and graph re-captures) rare
+                cap = max(new_rows, 2 * self.capacity, 512)
+                table = torch.full((cap, self.vocab_rows), -1, dtype=torch.int16, device=self.device)
+                dist = torch.zeros((cap,), dtype=torch.int16, device=self.device)
+                if self.rows:
+                    table[:self.rows] = self.table[:self.rows]
+                    dist[:self.rows] = self.dist[:self.rows]
+                self.table, self.dist, self.capacity = table, dist, cap
+                self.version += 1
+            self.table[base:new_rows] = torch.from_numpy(fsm.next).to(self.device)
+            self.dist[base:new_rows] = torch.from_numpy(fsm.dist).to(self.device)
+            self.rows = new_rows
+            self._bases[key] = base
+            self._fsms[key] = fsm
+            return base
+
+    def fsm(self, schema: Dict) -> CompiledFSM:
+        self.get(schema)
+        return self._fsms[self.key_of(schema)]
+
+    def start_dist(self, base: int) -> int:
+        return int(self.dist[base].item())
+
+    def signature(self) -> str:
+        return hashlib.sha1("|".join(sorted(self._bases)).encode()).hexdigest()[:12]

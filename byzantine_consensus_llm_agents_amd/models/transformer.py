@@ -1,0 +1,207 @@
+"""Tensor-parallel decoder (Qwen3 / Qwen2 / Mistral) over paged KV.
+
+One forward serves both phases:
+
+* prefill - packed variable-length prompts (``T = sum of uncached prompt
+  tokens``), attention over cached prefix + new tokens;
+* decode  - one token per sequence (``T = B``), captured into a HIP graph by
+  the engine.
+
+Per layer: fused residual-add+RMSNorm -> QKV GEMM (hipBLASLt)
+-> fused QK-norm+RoPE+paged-KV-write (HIP) -> paged attention (HIP, MFMA) ->
+o_proj GEMM [-> RCCL all-reduce] -> fused add+RMSNorm -> gate_up GEMM ->
+SiLU*mul (HIP) -> down GEMM [-> RCCL all-reduce].  Column-parallel
+QKV/gate_up, row-parallel o/down, vocab-parallel LM head + all-gather, so a
+TP group does 2L+1 collectives per forward like the reference's vLLM path.
+"""
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn.functional as F
+
+from .config import ModelConfig
+
+
+@dataclass
+class AttnMeta:
+    """Attention inputs of one forward (all device tensors)."""
+
+    positions: torch.Tensor      # [T] int32
+    slots: torch.Tensor          # [T] int32 (physical KV slot of each new token)
+    block_tables: torch.Tensor   # [B, max_blocks] int32
+    seq_lens: torch.Tensor       # [B] int32, tokens resident after this step
+    q_start: Optional[torch.Tensor] = None   # [B+1] int32 (prefill only)
+    max_q_len: int = 1
+    decode: bool = False
+    logits_idx: Optional[torch.Tensor] = None  # rows whose logits are needed
+
+
+class TPGroup:
+    """Thin wrapper over a torch.distributed process group (RCCL on ROCm)."""
+
+    def __init__(self, group=None, rank: int = 0, size: int = 1):
+        self.group, self.rank, self.size = group, rank, size
+
+    def all_reduce_(self, x: torch.Tensor) -> torch.Tensor:
+        if self.size > 1:
+            torch.distributed.all_reduce(x, group=self.group)
+        return x
+
+    def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
+        if self.size == 1:
+            return x
+        parts = [torch.empty_like(x) for _ in range(self.size)]
+        torch.distributed.all_gather(parts, x.contiguous(), group=self.group)
+        return torch.cat(parts, dim=-1)
+
+
+class DecoderModel:
+    def __init__(self, cfg: ModelConfig, ops, device, dtype=torch.bfloat16,
+                 tp: Optional[TPGroup] = None):
+        self.cfg = cfg
+        self.ops = ops
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.tp = tp or TPGroup()
+        ts = self.tp.size
+        if cfg.num_heads % ts or cfg.num_kv_heads % ts or cfg.intermediate_size % ts or cfg.vocab_size % ts:
+            raise ValueError(f"{cfg.name}: heads/intermediate/vocab not divisible by tp={ts}")
+        self.n_q = cfg.num_heads // ts
+        self.n_kv = cfg.num_kv_heads // ts
+        self.inter = cfg.intermediate_size // ts
+        self.vocab_local = cfg.vocab_size // ts
+        self.hd = cfg.head_dim
+        self.scale = cfg.head_dim ** -0.5
+        self.layers: List[Dict[str, torch.Tensor]] = []
+        self.embed: Optional[torch.Tensor] = None
+        self.lm_head: Optional[torch.Tensor] = None
+        self.final_norm: Optional[torch.Tensor] = None
+        self.cos_sin = None
+
+    # ------------------------------------------------------------- weights
+    def _shapes(self):
+        c, h = self.cfg, self.cfg.hidden_size
+        qkv_out = (self.n_q + 2 * self.n_kv) * self.hd
+        shapes = {"qkv": (qkv_out, h), "o": (h, self.n_q * self.hd), "gate_up": (2 * self.inter, h),
+                  "down": (h, self.inter), "ln1": (h,), "ln2": (h,)}
+        if c.qkv_bias:
+            shapes["qkv_bias"] = (qkv_out,)
+        if c.qk_norm:
+            shapes["q_norm"] = (self.hd,)
+            shapes["k_norm"] = (self.hd,)
+        return shapes
+
+    def init_random(self, seed: int = 0, std: float = 0.02):
+        """Random-init weights of this rank's shard directly on the device."""
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(seed * 1000003 + self.tp.rank)
+        c = self.cfg
+
+        def normal(*shape):
+            t = torch.empty(*shape, device=self.device, dtype=self.dtype)
+            t.normal_(0.0, std, generator=gen)
+            return t
+
+        def ones(*shape):
+            return torch.ones(*shape, device=self.device, dtype=self.dtype)
+
+        self.layers = []
+        for _ in range(c.num_layers):
+            layer = {}
+            for name, shape in self._shapes().items():
+                layer[name] = ones(*shape) if name in ("ln1", "ln2", "q_norm", "k_norm") else normal(*shape)
+            self.layers.append(layer)
+        # embedding replicated on every TP rank (1.5 GB bf16 at 152k x 5120); head vocab-parallel
+        g0 = torch.Generator(device=self.device)
+        g0.manual_seed(seed * 1000003 + 7)
+        self.embed = torch.empty(c.vocab_size, c.hidden_size, device=self.device, dtype=self.dtype)
+        self.embed.normal_(0.0, std, generator=g0)
+        if c.tie_embeddings:
+            lo = self.tp.rank * self.vocab_local
+            self.lm_head = self.embed[lo:lo + self.vocab_local]
+        else:
+            self.lm_head = normal(self.vocab_local, c.hidden_size)
+        self.final_norm = ones(c.hidden_size)
+        self._finish()
+
+    def load_hf_state_dict(self, sd: Dict[str, torch.Tensor]):
+        """Load (and TP-slice) an HF-named state dict (Qwen2/Qwen3/Mistral naming)."""
+        c, r = self.cfg, self.tp.rank
+        hd = self.hd
+
+        def get(name):
+            return sd[name].to(device=self.device, dtype=self.dtype)
+
+        def rows(t, n_local, per=1):
+            return t[r * n_local * per:(r + 1) * n_local * per]
+
+        self.layers = []
+        for i in range(c.num_layers):
+            p = f"model.layers.{i}."
+            q = rows(get(p + "self_attn.q_proj.weight"), self.n_q, hd)
+            k = rows(get(p + "self_attn.k_proj.weight"), self.n_kv, hd)
+            v = rows(get(p + "self_attn.v_proj.weight"), self.n_kv, hd)
+            layer = {"qkv": torch.cat([q, k, v]).contiguous(),
+                     "o": get(p + "self_attn.o_proj.weight")[:, r * self.n_q * hd:(r + 1) * self.n_q * hd].contiguous(),
+                     "gate_up": torch.cat([rows(get(p + "mlp.gate_proj.weight"), self.inter),
+                                           rows(get(p + "mlp.up_proj.weight"), self.inter)]).contiguous(),
+                     "down": get(p + "mlp.down_proj.weight")[:, r * self.inter:(r + 1) * self.inter].contiguous(),
+                     "ln1": get(p + "input_layernorm.weight"),
+                     "ln2": get(p + "post_attention_layernorm.weight")}
+            if c.qkv_bias:
+                layer["qkv_bias"] = torch.cat([rows(get(p + "self_attn.q_proj.bias"), self.n_q, hd),
+                                               rows(get(p + "self_attn.k_proj.bias"), self.n_kv, hd),
+                                               rows(get(p + "self_attn.v_proj.bias"), self.n_kv, hd)])
+            if c.qk_norm:
+                layer["q_norm"] = get(p + "self_attn.q_norm.weight")
+                layer["k_norm"] = get(p + "self_attn.k_norm.weight")
+            self.layers.append(layer)
+        self.embed = get("model.embed_tokens.weight")
+        head = self.embed if c.tie_embeddings or "lm_head.weight" not in sd else get("lm_head.weight")
+        self.lm_head = rows(head, self.vocab_local).contiguous()
+        self.final_norm = get("model.norm.weight")
+        self._finish()
+
+    def _finish(self):
+        from ..ops.reference import rope_cache
+        c = self.cfg
+        self.cos_sin = rope_cache(min(c.max_position, 65536), self.hd, c.rope_theta, self.device)
+
+    def weight_bytes(self) -> int:
+        n = sum(t.numel() * t.element_size() for layer in self.layers for t in layer.values())
+        n += self.embed.numel() * self.embed.element_size()
+        if not self.cfg.tie_embeddings:
+            n += self.lm_head.numel() * self.lm_head.element_size()
+        return n
+
+    # ------------------------------------------------------------- forward
+    def forward(self, tokens: torch.Tensor, meta: AttnMeta, k_cache: torch.Tensor,
+                v_cache: torch.Tensor) -> torch.Tensor:
+        """Returns logits ``[len(logits_idx) or B, vocab]`` (full vocab, fp32 or bf16)."""
+        ops, c = self.ops, self.cfg
+        x = F.embedding(tokens.long(), self.embed)
+        residual = None
+        for li, L in enumerate(self.layers):
+            h, residual = ops.add_rmsnorm(x, residual, L["ln1"], c.rms_eps)
+            qkv = F.linear(h, L["qkv"], L.get("qkv_bias"))
+            q = ops.qk_norm_rope_kv_write(qkv, meta.positions, meta.slots, self.n_q, self.n_kv, self.hd,
+                                          L.get("q_norm"), L.get("k_norm"), c.rms_eps, self.cos_sin,
+                                          k_cache, v_cache, li)
+            if meta.decode:
+                attn = ops.paged_attention_decode(q, k_cache, v_cache, li, meta.block_tables,
+                                                  meta.seq_lens, self.scale)
+            else:
+                attn = ops.paged_attention_prefill(q, k_cache, v_cache, li, meta.block_tables,
+                                                   meta.q_start, meta.seq_lens, self.scale, meta.max_q_len)
+            x = self.tp.all_reduce_(F.linear(attn, L["o"]))
+            h, residual = ops.add_rmsnorm(x, residual, L["ln2"], c.rms_eps)
+            gu = F.linear(h, L["gate_up"])
+            x = self.tp.all_reduce_(F.linear(ops.silu_mul(gu), L["down"]))
+        if meta.logits_idx is not None:
+            x = x.index_select(0, meta.logits_idx)
+            residual = residual.index_select(0, meta.logits_idx)
+        h, _ = ops.add_rmsnorm(x, residual, self.final_norm, c.rms_eps)
+        logits = F.linear(h, self.lm_head)
+        return self.tp.all_gather_last(logits)

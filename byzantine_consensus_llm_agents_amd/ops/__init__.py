@@ -1,0 +1,48 @@
+"""Op dispatch: ``get_ops("hip")`` -> HIP/CDNA4 kernels, ``get_ops("torch")`` -> references.
+
+Both namespaces expose the same functions (see ``reference.py`` for the
+semantics).  The HIP namespace raises at import when ``libbcg_kernels.so``
+is missing instead of silently falling back.
+"""
+
+from types import SimpleNamespace
+
+import torch
+
+from . import reference as _ref
+
+
+def _torch_ops() -> SimpleNamespace:
+    def decode(q, k_cache, v_cache, layer, block_tables, seq_lens, scale):
+        B = q.shape[0]
+        q_start = torch.arange(B + 1, dtype=torch.int32, device=q.device)
+        return _ref.paged_attention(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale)
+
+    def prefill(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale, max_q_len=None):
+        return _ref.paged_attention(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale)
+
+    return SimpleNamespace(
+        name="torch",
+        rmsnorm=_ref.rmsnorm,
+        add_rmsnorm=_ref.add_rmsnorm,
+        qk_norm_rope_kv_write=_ref.qk_norm_rope_kv_write,
+        paged_attention_decode=decode,
+        paged_attention_prefill=prefill,
+        silu_mul=_ref.silu_mul,
+        sample_step=_ref.sample_step,
+    )
+
+
+_CACHE = {}
+
+
+def get_ops(backend: str) -> SimpleNamespace:
+    if backend not in _CACHE:
+        if backend == "torch":
+            _CACHE[backend] = _torch_ops()
+        elif backend == "hip":
+            from .hip import hip_ops
+            _CACHE[backend] = hip_ops()
+        else:
+            raise ValueError(f"unknown ops backend {backend!r}")
+    return _CACHE[backend]
