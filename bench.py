@@ -1,0 +1,218 @@
+"""Headline benchmark: agent decisions/sec (node), 8 honest + 2 Byzantine BCG, Qwen3-14B bf16.
+
+Metric (BASELINE.md "Measurement protocol"): accepted decide outputs +
+accepted vote outputs per wall-clock second, summed over every GPU of the
+node.  One "step" = one BCG round of every simulation running on the GPU:
+all agents' decide prompts in ONE engine call, all vote prompts in ONE call,
+plus whatever retries the reference's retry ladder triggers.
+
+Layout: one process per GPU (torchrun), data-parallel over independent
+simulation seeds (``--sims-per-gpu`` games share each GPU's engine; a game
+that ends is replaced by a fresh seed so the pool stays full).  With
+``--tp > 1`` groups of GPUs form tensor-parallel engines (RCCL all-reduce).
+
+Data: random-init weights of the real architecture and the synthetic
+byte-level BPE tokenizer (no network for checkpoints); the budget-aware JSON
+grammar guarantees schema-valid outputs from untrained weights, at the full
+max_tokens (300 decide / 200 vote) -- a pessimistic decode length.
+
+Timing: W warmup rounds, barrier + cuda.synchronize, K timed rounds,
+barrier + synchronize; the max time over ranks; rank 0 prints one JSON line.
+"""
+
+import argparse
+import json
+import os
+import random
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+BASELINE_VALUE = None  # the reference publishes no number
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3, help="timed BCG rounds")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed BCG rounds")
+    ap.add_argument("--model", default="qwen3-14b")
+    ap.add_argument("--honest", type=int, default=8)
+    ap.add_argument("--byzantine", type=int, default=2)
+    ap.add_argument("--sims-per-gpu", type=int, default=16)
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--max-rounds", type=int, default=50)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--backend", default="hip")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-prefix-cache", action="store_true")
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args()
+
+
+class SimPool:
+    """S simulations advanced in lock-step; each round's engine calls are coalesced."""
+
+    def __init__(self, llm, n_sims, honest, byzantine, max_rounds, seed, rank):
+        from byzantine_consensus_llm_agents_amd.bcg.simulation import BCGSimulation
+        self.BCGSimulation = BCGSimulation
+        self.llm = llm
+        self.honest, self.byzantine, self.max_rounds = honest, byzantine, max_rounds
+        self.seed_base = seed * 100003 + rank * 7919
+        self.next_seed = 0
+        self.sims = [self._new_sim() for _ in range(n_sims)]
+        self.games_finished = 0
+        self.outcomes = {}
+
+    def _new_sim(self):
+        self.next_seed += 1
+        return self.BCGSimulation(self.honest, self.byzantine, config={
+            "max_rounds": self.max_rounds, "value_range": (0, 50), "consensus_threshold": 66.0,
+            "verbose": False, "byzantine_awareness": "may_exist", "seed": self.seed_base + self.next_seed})
+
+    def counts(self):
+        return sum(s.counters["decisions_accepted"] + s.counters["votes_accepted"] for s in self.sims)
+
+    def round(self):
+        """One round of every simulation; returns decisions accepted in it."""
+        before = self.counts()
+        errors = []
+
+        def work(sim):
+            try:
+                sim.run_round()
+            except BaseException as exc:  # surface thread failures
+                errors.append(exc)
+            finally:
+                self.llm.unregister_client()
+
+        for _ in self.sims:
+            self.llm.register_client()
+        threads = [threading.Thread(target=work, args=(s,)) for s in self.sims]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        if errors:
+            raise errors[0]
+        made = self.counts() - before
+        for i, s in enumerate(self.sims):
+            if s.game.game_over:
+                stats = s.game.get_statistics()
+                o = stats.get("consensus_outcome")
+                self.outcomes[o] = self.outcomes.get(o, 0) + 1
+                self.games_finished += 1
+                self.sims[i] = self._new_sim()
+        return made
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend == "hip":
+        torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl" if args.backend == "hip" else "gloo")
+
+    from byzantine_consensus_llm_agents_amd.bcg import config as C
+    from byzantine_consensus_llm_agents_amd.bcg.engine_agent import EngineAgent
+    from byzantine_consensus_llm_agents_amd.engine.llm import LLM
+    from byzantine_consensus_llm_agents_amd.models.config import ALIASES
+
+    model = ALIASES.get(args.model, args.model)
+    C.METRICS_CONFIG["save_results"] = False
+    C.VLLM_CONFIG["model_name"] = model
+    C.VLLM_CONFIG["tensor_parallel_size"] = args.tp
+    C.ENGINE_CONFIG.update(backend=args.backend, budget_aware_json=True, seed=args.seed + rank // args.tp,
+                           use_hip_graphs=not args.no_graphs, prefix_caching=not args.no_prefix_cache)
+    C.BCG_CONFIG["value_range"] = (0, 50)
+    random.seed(args.seed + rank)
+
+    t0 = time.perf_counter()
+    llm = LLM(model, max_model_len=C.VLLM_CONFIG["max_model_len"],
+              gpu_memory_utilization=C.VLLM_CONFIG["gpu_memory_utilization"],
+              tensor_parallel_size=args.tp, backend=args.backend, seed=args.seed + rank // args.tp)
+    # share the engine with every agent (same model name + config => no reload)
+    EngineAgent._shared_llm = llm
+    EngineAgent._shared_model_name = model
+    EngineAgent._shared_model_config = dict(C.VLLM_CONFIG)
+    init_s = time.perf_counter() - t0
+
+    pool = SimPool(llm, args.sims_per_gpu, args.honest, args.byzantine, args.max_rounds,
+                   args.seed + rank // args.tp, rank // args.tp)
+    for i in range(args.warmup):
+        n = pool.round()
+        if rank == 0 and args.verbose:
+            print(f"[warmup {i}] decisions={n}", file=sys.stderr, flush=True)
+
+    eng = getattr(llm.backend, "stats", {})
+    stats0 = dict(eng)
+    if world > 1:
+        dist.barrier()
+    if args.backend == "hip":
+        torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    decisions = 0
+    for i in range(args.steps):
+        n = pool.round()
+        decisions += n
+        if rank == 0:
+            print(f"[round {i}] decisions={n} elapsed={time.perf_counter() - t_start:.2f}s",
+                  file=sys.stderr, flush=True)
+    if args.backend == "hip":
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+
+    # DP groups: only one rank per TP group contributes decisions
+    mine = decisions if rank % args.tp == 0 else 0
+    if world > 1:
+        t = torch.tensor([mine, elapsed], dtype=torch.float64,
+                         device="cuda" if args.backend == "hip" else "cpu")
+        tot = t.clone()
+        dist.all_reduce(tot[:1], op=dist.ReduceOp.SUM)
+        mx = t[1:].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        total_decisions, elapsed = float(tot[0]), float(mx[0])
+    else:
+        total_decisions = float(mine)
+    value = total_decisions / elapsed if elapsed > 0 else 0.0
+    d_eng = {k: eng.get(k, 0) - stats0.get(k, 0) for k in eng}
+    if rank == 0:
+        line = {
+            "metric": "agent decisions/sec (node), 8h+2b BCG Qwen3-14B; consensus-rate parity",
+            "value": round(value, 3), "unit": "decisions/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / max(args.steps, 1), 2),
+            "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": "bf16",
+            "data": "synthetic (random-init weights, synthetic BPE tokenizer, budget-aware JSON grammar)",
+            "config": {"model": model, "honest": args.honest, "byzantine": args.byzantine,
+                       "global_batch": args.sims_per_gpu * (args.honest + args.byzantine) * (world // args.tp),
+                       "sims_per_gpu": args.sims_per_gpu, "seq_len": C.VLLM_CONFIG["max_model_len"],
+                       "max_tokens_decide": C.LLM_CONFIG["max_tokens_decide"],
+                       "max_tokens_vote": C.LLM_CONFIG["max_tokens_vote"],
+                       "parallelism": f"dp{world // args.tp}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
+                       "hip_graphs": not args.no_graphs, "prefix_caching": not args.no_prefix_cache},
+            "detail": {"decisions": total_decisions, "elapsed_s": round(elapsed, 3), "init_s": round(init_s, 1),
+                       "engine_per_rank": d_eng, "games_finished_rank0": pool.games_finished,
+                       "outcomes_rank0": pool.outcomes,
+                       "phases_rank0": llm.backend.timer.summary() if hasattr(llm.backend, "timer") else {}},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

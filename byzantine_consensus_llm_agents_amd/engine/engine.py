@@ -164,9 +164,11 @@ class InferenceEngine:
         else:
             budget = 256 * 2 ** 20
         num_blocks = max(16, min(budget // per_block, want_tokens // bs + 1))
-        shape = (m.cfg.num_layers, num_blocks, m.n_kv, bs, m.hd)
-        self.k_cache = torch.zeros(shape, dtype=a.dtype, device=self.device)
-        self.v_cache = torch.zeros(shape, dtype=a.dtype, device=self.device)
+        self.k_cache = torch.zeros((m.cfg.num_layers, num_blocks, m.n_kv, bs, m.hd), dtype=a.dtype,
+                                   device=self.device)
+        # V is stored transposed per block-head (see ops/reference.py)
+        self.v_cache = torch.zeros((m.cfg.num_layers, num_blocks, m.n_kv, m.hd, bs), dtype=a.dtype,
+                                   device=self.device)
         from ..runtime import BlockManager
         # block 0 is scratch (padding rows of graph buckets write there); never handed out
         self.blocks = BlockManager(num_blocks - 1, bs)
@@ -315,7 +317,14 @@ class InferenceEngine:
             if b == len(s.prompt_ids):
                 last_idx.append(q_start[-1] - 1)
                 last_rows.append(r)
+        # 64-query tiles for the HIP prefill kernel, deepest (most keys) first
+        tiles = []
+        for i, (r, a, b) in enumerate(chunk):
+            for t in range(q_start[i], q_start[i + 1], 64):
+                tiles.append((b - (q_start[i + 1] - t), i, t, min(t + 64, q_start[i + 1])))
+        tiles.sort(key=lambda x: -x[0])
         meta = AttnMeta(
+            tiles=torch.tensor([x[1:] for x in tiles], dtype=torch.int32, device=dev),
             positions=torch.cat(pos).to(torch.int32).to(dev),
             slots=torch.cat(slots).to(torch.int32).to(dev),
             block_tables=table_cpu[rows].to(dev),

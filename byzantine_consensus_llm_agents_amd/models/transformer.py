@@ -36,6 +36,7 @@ class AttnMeta:
     max_q_len: int = 1
     decode: bool = False
     logits_idx: Optional[torch.Tensor] = None  # rows whose logits are needed
+    tiles: Optional[torch.Tensor] = None       # [n_tiles, 3] int32 prefill work list (HIP kernel)
 
 
 class TPGroup:
@@ -194,7 +195,8 @@ class DecoderModel:
                                                   meta.seq_lens, self.scale)
             else:
                 attn = ops.paged_attention_prefill(q, k_cache, v_cache, li, meta.block_tables,
-                                                   meta.q_start, meta.seq_lens, self.scale, meta.max_q_len)
+                                                   meta.q_start, meta.seq_lens, self.scale, meta.max_q_len,
+                                                   meta.tiles)
             x = self.tp.all_reduce_(F.linear(attn, L["o"]))
             h, residual = ops.add_rmsnorm(x, residual, L["ln2"], c.rms_eps)
             gu = F.linear(h, L["gate_up"])

@@ -18,7 +18,7 @@ def _torch_ops() -> SimpleNamespace:
         q_start = torch.arange(B + 1, dtype=torch.int32, device=q.device)
         return _ref.paged_attention(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale)
 
-    def prefill(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale, max_q_len=None):
+    def prefill(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale, max_q_len=None, tiles=None):
         return _ref.paged_attention(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale)
 
     return SimpleNamespace(

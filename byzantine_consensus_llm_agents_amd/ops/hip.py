@@ -1,0 +1,169 @@
+"""ctypes bindings of ``libbcg_kernels.so`` (csrc/kernels, gfx950).
+
+Every wrapper validates dtypes, contiguity and shapes on the host before it
+launches (a kernel that indexes out of bounds can take down every GPU of the
+node), then launches on the current HIP stream -- so the calls are captured
+by ``torch.cuda.graph`` like any PyTorch op.  A missing library raises: on a
+GPU box the engine never silently falls back to the PyTorch references.
+"""
+
+import ctypes
+import os
+from types import SimpleNamespace
+
+import torch
+
+from ..utils.build import kernels_target
+
+_LIB = None
+
+c_int, c_float, c_void_p, c_uint32, c_int64 = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int64
+
+
+def load_library(path: str = None) -> ctypes.CDLL:
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = path or kernels_target()
+    if not os.path.exists(path):
+        raise RuntimeError(f"HIP kernel library not found at {path}; run `python -m "
+                           "byzantine_consensus_llm_agents_amd.utils.build` (hipcc --offload-arch=gfx950)")
+    lib = ctypes.CDLL(path)
+    sig = {
+        "bcg_add_rmsnorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_int, c_void_p],
+        "bcg_silu_mul": [c_void_p, c_void_p, c_int64, c_int, c_void_p],
+        "bcg_qk_norm_rope_kv_write": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                      c_float, c_void_p],
+        "bcg_paged_attention_decode": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
+                                       c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int,
+                                       c_void_p, c_void_p],
+        "bcg_paged_attention_prefill": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
+                                        c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
+                                        c_void_p, c_void_p],
+        "bcg_guided_sample": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                              c_uint32, c_int, c_int, c_int, c_int, c_void_p],
+    }
+    for name, argtypes in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = c_int
+    _LIB = lib
+    return lib
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t: torch.Tensor):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _check(rc: int, name: str):
+    if rc != 0:
+        raise RuntimeError(f"{name} launch failed (rc={rc})")
+
+
+def _req(cond: bool, msg: str):
+    if not cond:
+        raise ValueError(msg)
+
+
+def hip_ops() -> SimpleNamespace:
+    lib = load_library()
+    SPLIT = 256
+
+    def add_rmsnorm(x, residual, w, eps):
+        _req(x.dtype == torch.bfloat16 and x.is_contiguous() and x.dim() == 2, "add_rmsnorm: x bf16 [T,H]")
+        T, H = x.shape
+        _req(w.shape == (H,) and w.dtype == torch.bfloat16, "add_rmsnorm: weight [H] bf16")
+        has_res = residual is not None
+        if not has_res:
+            residual = torch.empty_like(x)
+        else:
+            _req(residual.shape == x.shape and residual.is_contiguous(), "add_rmsnorm: residual shape")
+        out = torch.empty_like(x)
+        _check(lib.bcg_add_rmsnorm(_p(x), _p(residual), _p(w), _p(out), T, H, eps, int(has_res), _stream()),
+               "add_rmsnorm")
+        return out, residual
+
+    def rmsnorm(x, w, eps):
+        out, _ = add_rmsnorm(x, None, w, eps)
+        return out
+
+    def silu_mul(gu):
+        _req(gu.dtype == torch.bfloat16 and gu.is_contiguous() and gu.dim() == 2, "silu_mul: bf16 [T,2I]")
+        T, I2 = gu.shape
+        out = torch.empty(T, I2 // 2, dtype=gu.dtype, device=gu.device)
+        _check(lib.bcg_silu_mul(_p(gu), _p(out), T, I2 // 2, _stream()), "silu_mul")
+        return out
+
+    def qk_norm_rope_kv_write(qkv, positions, slots, n_q, n_kv, head_dim, q_norm, k_norm, eps, cos_sin,
+                              k_cache, v_cache, layer):
+        T = qkv.shape[0]
+        _req(qkv.is_contiguous() and qkv.shape[1] == (n_q + 2 * n_kv) * head_dim, "qkv shape")
+        _req(positions.dtype == torch.int32 and slots.dtype == torch.int32 and positions.numel() == T
+             and slots.numel() == T, "positions/slots int32 [T]")
+        _req(cos_sin.dtype == torch.float32 and cos_sin.shape[1] == head_dim, "cos_sin table")
+        L, NB, nkv_c, BS, hd = k_cache.shape
+        _req(nkv_c == n_kv and hd == head_dim and v_cache.shape == (L, NB, n_kv, hd, BS), "kv cache layout")
+        q = torch.empty(T, n_q, head_dim, dtype=qkv.dtype, device=qkv.device)
+        _check(lib.bcg_qk_norm_rope_kv_write(
+            _p(qkv), _p(positions), _p(slots), _p(q), _p(q_norm) if q_norm is not None else None,
+            _p(k_norm) if k_norm is not None else None, _p(cos_sin), _p(k_cache), _p(v_cache), layer, T,
+            n_q, n_kv, head_dim, NB, BS, eps, _stream()), "qk_norm_rope_kv_write")
+        return q
+
+    def paged_attention_decode(q, k_cache, v_cache, layer, block_tables, seq_lens, scale):
+        B, n_q, hd = q.shape
+        L, NB, n_kv, BS, _ = k_cache.shape
+        _req(q.is_contiguous() and block_tables.dtype == torch.int32 and block_tables.is_contiguous()
+             and block_tables.shape[0] == B and seq_lens.numel() == B, "decode attention inputs")
+        max_blocks = block_tables.shape[1]
+        max_splits = (max_blocks * BS + SPLIT - 1) // SPLIT
+        ws = torch.empty(B * n_q * max_splits * (hd + 2), dtype=torch.float32, device=q.device)
+        out = torch.empty(B, n_q * hd, dtype=q.dtype, device=q.device)
+        _check(lib.bcg_paged_attention_decode(
+            _p(q), _p(k_cache), _p(v_cache), layer, NB, n_kv, _p(block_tables), max_blocks, _p(seq_lens),
+            B, n_q, hd, BS, scale, _p(ws), max_splits, _p(out), _stream()), "paged_attention_decode")
+        return out
+
+    def paged_attention_prefill(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale,
+                                max_q_len=None, tiles=None):
+        T, n_q, hd = q.shape
+        L, NB, n_kv, BS, _ = k_cache.shape
+        _req(tiles is not None and tiles.dtype == torch.int32 and tiles.dim() == 2 and tiles.shape[1] == 3,
+             "prefill attention needs the [n_tiles,3] int32 tile table")
+        _req(q.is_contiguous() and block_tables.dtype == torch.int32 and q_start.dtype == torch.int32
+             and seq_lens.dtype == torch.int32, "prefill attention inputs")
+        out = torch.empty(T, n_q * hd, dtype=q.dtype, device=q.device)
+        _check(lib.bcg_paged_attention_prefill(
+            _p(q), _p(k_cache), _p(v_cache), layer, NB, n_kv, _p(block_tables), block_tables.shape[1],
+            _p(q_start), _p(seq_lens), _p(tiles), tiles.shape[0], n_q, hd, BS, scale, _p(out), _stream()),
+            "paged_attention_prefill")
+        return out
+
+    def sample_step(logits, fsm_next, fsm_dist, fsm_base, fsm_state, gen_count, max_new, temperature,
+                    row_keys, done, seq_lens, out_tokens, next_tokens, seed, budget_aware, n_text_tokens,
+                    eos_id, eos_id2):
+        B, V = logits.shape
+        _req(logits.dtype == torch.bfloat16 and logits.is_contiguous(), "logits bf16 [B,V]")
+        _req(fsm_next.dtype == torch.int16 and fsm_next.shape[1] == V and fsm_dist.dtype == torch.int16,
+             "fsm tables int16 [rows,V]")
+        for t in (fsm_base, fsm_state, gen_count, max_new, row_keys, done, seq_lens, next_tokens):
+            _req(t.dtype == torch.int32 and t.numel() == B and t.is_contiguous(), "per-row int32 state")
+        _req(temperature.dtype == torch.float32 and out_tokens.dtype == torch.int32
+             and out_tokens.shape[0] == B, "temperature/out_tokens")
+        _check(lib.bcg_guided_sample(
+            _p(logits), B, V, _p(fsm_next), _p(fsm_dist), _p(fsm_base), _p(fsm_state), _p(gen_count),
+            _p(max_new), _p(temperature), _p(row_keys), _p(done), _p(seq_lens), _p(out_tokens),
+            out_tokens.shape[1], _p(next_tokens), seed & 0xFFFFFFFF, int(bool(budget_aware)), n_text_tokens,
+            eos_id, eos_id2, _stream()), "guided_sample")
+
+    return SimpleNamespace(name="hip", rmsnorm=rmsnorm, add_rmsnorm=add_rmsnorm, silu_mul=silu_mul,
+                           qk_norm_rope_kv_write=qk_norm_rope_kv_write,
+                           paged_attention_decode=paged_attention_decode,
+                           paged_attention_prefill=paged_attention_prefill, sample_step=sample_step,
+                           library=lib)

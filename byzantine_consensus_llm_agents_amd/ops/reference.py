@@ -4,8 +4,10 @@ These define the semantics the HIP kernels in ``csrc/kernels`` must match and
 run the ``torch`` backend (CPU tests).  Layout conventions shared with the
 kernels:
 
-* KV cache: ``k_cache, v_cache : [L, num_blocks, n_kv, block_size, head_dim]``
-  (bf16); block 0 is a never-allocated scratch block.
+* KV cache: ``k_cache : [L, num_blocks, n_kv, block_size, head_dim]`` and
+  ``v_cache : [L, num_blocks, n_kv, head_dim, block_size]`` (V stored
+  transposed per block-head: it is the A operand of ``O^T = V^T P^T`` in the
+  MFMA attention kernels); bf16; block 0 is a never-allocated scratch block.
 * ``block_tables : [B, max_blocks] int32``; ``seq_lens : [B] int32`` = number
   of tokens whose KV is resident *including* the tokens of this step.
 * Sampling: Gumbel-max with a counter-based hash (``gumbel_hash``) so the
@@ -73,15 +75,18 @@ def qk_norm_rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, slots: tor
     blk = (slots // bs).long()
     off = (slots % bs).long()
     k_cache[layer, blk, :, off] = k.to(k_cache.dtype)
-    v_cache[layer, blk, :, off] = v.to(v_cache.dtype)
+    v_cache[layer, blk, :, :, off] = v.to(v_cache.dtype)
     return q.to(qkv.dtype)
 
 
-def _gather_kv(cache, layer, table_row, ctx):
-    bs = cache.shape[3]
+def _gather_kv(cache, layer, table_row, ctx, transposed=False):
+    blocks = cache[layer]
+    if transposed:                                        # V: [NB, n_kv, hd, bs]
+        blocks = blocks.transpose(2, 3)
+    bs = blocks.shape[2]
     nblk = (ctx + bs - 1) // bs
-    blocks = cache[layer, table_row[:nblk].long()]          # [nblk, n_kv, bs, hd]
-    return blocks.permute(1, 0, 2, 3).reshape(cache.shape[2], nblk * bs, cache.shape[4])[:, :ctx]
+    sel = blocks[table_row[:nblk].long()]                  # [nblk, n_kv, bs, hd]
+    return sel.permute(1, 0, 2, 3).reshape(sel.shape[1], nblk * bs, sel.shape[3])[:, :ctx]
 
 
 def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, layer: int,
@@ -103,7 +108,7 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
             continue
         ctx = int(seq_lens[b])
         k = _gather_kv(k_cache, layer, block_tables[b], ctx).float()   # [n_kv, ctx, hd]
-        v = _gather_kv(v_cache, layer, block_tables[b], ctx).float()
+        v = _gather_kv(v_cache, layer, block_tables[b], ctx, transposed=True).float()
         k = k.repeat_interleave(group, 0)
         v = v.repeat_interleave(group, 0)
         qb = q[s:e].float().permute(1, 0, 2)                            # [n_q, qlen, hd]

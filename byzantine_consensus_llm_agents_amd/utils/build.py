@@ -63,6 +63,7 @@ def build_runtime(force: bool = False, verbose: bool = False) -> str:
     out = _run(cmd)
     if verbose and out:
         print(out)
+    os.chmod(tmp, 0o755)
     os.replace(tmp, target)
     return target
 
@@ -86,6 +87,7 @@ def build_kernels(force: bool = False, verbose: bool = False) -> str:
     out = _run(cmd)
     if verbose and out:
         print(out)
+    os.chmod(tmp, 0o755)
     os.replace(tmp, target)
     return target
 

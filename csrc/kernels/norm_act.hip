@@ -1,0 +1,105 @@
+// Row-wise RMSNorm with fused residual add, and SiLU-and-mul.
+//
+// add_rmsnorm: one workgroup (256 threads = 4 wave64) per row; every thread
+// owns up to MAX_CHUNK 16-byte chunks (8 bf16) kept in registers, so the row
+// is read once and written twice (residual + normed) -- the HBM minimum for
+// the fused op.  Sum of squares: wave shuffle reduce, then 4 partials via LDS.
+//
+// silu_mul: grid-stride over 8-element vectors of [T, 2I] -> [T, I].
+
+#include "common.h"
+
+namespace {
+
+constexpr int NORM_THREADS = 256;
+constexpr int MAX_CHUNK = 4;  // H <= 256 * 8 * 4 = 8192
+
+__global__ __launch_bounds__(NORM_THREADS) void add_rmsnorm_kernel(
+    const bf16_t* __restrict__ x, bf16_t* __restrict__ residual, const bf16_t* __restrict__ w,
+    bf16_t* __restrict__ out, int H, float eps, int has_residual) {
+  const int row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int nvec = H / 8;
+  const size_t base = static_cast<size_t>(row) * H;
+  float v[MAX_CHUNK][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAX_CHUNK; ++c) {
+    const int vi = tid + c * NORM_THREADS;
+    if (vi < nvec) {
+      u16x8 xv = *reinterpret_cast<const u16x8*>(x + base + vi * 8);
+      u16x8 rv;
+      if (has_residual) rv = *reinterpret_cast<const u16x8*>(residual + base + vi * 8);
+      u16x8 nr;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float f = bf2f(xv[j]);
+        if (has_residual) f += bf2f(rv[j]);
+        nr[j] = f2bf(f);
+        f = bf2f(nr[j]);  // normalise the value actually stored (matches the reference)
+        v[c][j] = f;
+        ss += f * f;
+      }
+      *reinterpret_cast<u16x8*>(residual + base + vi * 8) = nr;
+    }
+  }
+  __shared__ float partial[NORM_THREADS / WAVE];
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) partial[tid >> 6] = ss;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int i = 0; i < NORM_THREADS / WAVE; ++i) tot += partial[i];
+  const float inv = rsqrtf(tot / H + eps);
+#pragma unroll
+  for (int c = 0; c < MAX_CHUNK; ++c) {
+    const int vi = tid + c * NORM_THREADS;
+    if (vi < nvec) {
+      u16x8 wv = *reinterpret_cast<const u16x8*>(w + vi * 8);
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[c][j] * inv * bf2f(wv[j]));
+      *reinterpret_cast<u16x8*>(out + base + vi * 8) = o;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void silu_mul_kernel(const bf16_t* __restrict__ gu,
+                                                       bf16_t* __restrict__ out, int64_t T, int I) {
+  const int64_t nvec_row = I / 8;
+  const int64_t total = T * nvec_row;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t r = i / nvec_row, c = i % nvec_row;
+    const bf16_t* g = gu + r * 2 * I + c * 8;
+    u16x8 gv = *reinterpret_cast<const u16x8*>(g);
+    u16x8 uv = *reinterpret_cast<const u16x8*>(g + I);
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float a = bf2f(gv[j]);
+      o[j] = f2bf(a / (1.f + __expf(-a)) * bf2f(uv[j]));
+    }
+    *reinterpret_cast<u16x8*>(out + r * I + c * 8) = o;
+  }
+}
+
+}  // namespace
+
+BCG_API int bcg_add_rmsnorm(const void* x, void* residual, const void* w, void* out, int T, int H,
+                            float eps, int has_residual, hipStream_t stream) {
+  if (H % 8 != 0 || H > NORM_THREADS * 8 * MAX_CHUNK || T <= 0) return -2;
+  hipLaunchKernelGGL(add_rmsnorm_kernel, dim3(T), dim3(NORM_THREADS), 0, stream,
+                     static_cast<const bf16_t*>(x), static_cast<bf16_t*>(residual),
+                     static_cast<const bf16_t*>(w), static_cast<bf16_t*>(out), H, eps, has_residual);
+  return BCG_CHECK_LAUNCH();
+}
+
+BCG_API int bcg_silu_mul(const void* gu, void* out, int64_t T, int I, hipStream_t stream) {
+  if (I % 8 != 0 || T <= 0) return -2;
+  const int64_t work = T * (I / 8);
+  const int blocks = static_cast<int>(std::min<int64_t>((work + 255) / 256, 256 * 16));
+  hipLaunchKernelGGL(silu_mul_kernel, dim3(blocks), dim3(256), 0, stream,
+                     static_cast<const bf16_t*>(gu), static_cast<bf16_t*>(out), T, I);
+  return BCG_CHECK_LAUNCH();
+}

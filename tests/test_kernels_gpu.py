@@ -1,0 +1,165 @@
+"""HIP kernel numerics vs the fp32 PyTorch references (ops/reference.py). GPU only."""
+import math
+
+import pytest
+import torch
+
+from byzantine_consensus_llm_agents_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hip():
+    from byzantine_consensus_llm_agents_amd.ops import get_ops
+    return get_ops("hip")
+
+
+def _close(a, b, atol, rtol=2e-2):
+    torch.testing.assert_close(a.float(), b.float(), atol=atol, rtol=rtol)
+
+
+@pytest.mark.parametrize("H,has_res", [(5120, True), (5120, False), (896, True), (6144, True)])
+def test_add_rmsnorm(hip, H, has_res):
+    torch.manual_seed(0)
+    x = torch.randn(37, H, device="cuda", dtype=torch.bfloat16)
+    w = (torch.rand(H, device="cuda") + 0.5).to(torch.bfloat16)
+    res = torch.randn(37, H, device="cuda", dtype=torch.bfloat16) if has_res else None
+    y_ref, r_ref = R.add_rmsnorm(x, None if res is None else res.clone(), w, 1e-6)
+    y, r = hip.add_rmsnorm(x, None if res is None else res.clone(), w, 1e-6)
+    _close(r, r_ref, atol=0, rtol=0)
+    _close(y, y_ref, atol=2e-2)
+
+
+def test_silu_mul(hip):
+    gu = torch.randn(19, 2 * 17408, device="cuda", dtype=torch.bfloat16)
+    _close(hip.silu_mul(gu), R.silu_mul(gu), atol=2e-2)
+
+
+def _caches(L, NB, n_kv, hd, BS=16, fill=True):
+    k = torch.randn(L, NB, n_kv, BS, hd, device="cuda", dtype=torch.bfloat16) if fill else \
+        torch.zeros(L, NB, n_kv, BS, hd, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(L, NB, n_kv, hd, BS, device="cuda", dtype=torch.bfloat16) if fill else \
+        torch.zeros(L, NB, n_kv, hd, BS, device="cuda", dtype=torch.bfloat16)
+    return k, v
+
+
+@pytest.mark.parametrize("n_q,n_kv,hd,qk_norm", [(40, 8, 128, True), (14, 2, 64, False), (48, 8, 128, False)])
+def test_qk_norm_rope_kv_write(hip, n_q, n_kv, hd, qk_norm):
+    torch.manual_seed(1)
+    T, L, NB = 29, 2, 12
+    qkv = torch.randn(T, (n_q + 2 * n_kv) * hd, device="cuda", dtype=torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), device="cuda", dtype=torch.int32)
+    slots = torch.randperm(NB * 16, device="cuda")[:T].to(torch.int32)
+    qn = (torch.rand(hd, device="cuda") + 0.5).to(torch.bfloat16) if qk_norm else None
+    kn = (torch.rand(hd, device="cuda") + 0.5).to(torch.bfloat16) if qk_norm else None
+    cs = R.rope_cache(8192, hd, 1e6, "cuda")
+    k1, v1 = _caches(L, NB, n_kv, hd, fill=False)
+    k2, v2 = _caches(L, NB, n_kv, hd, fill=False)
+    q_ref = R.qk_norm_rope_kv_write(qkv, pos, slots, n_q, n_kv, hd, qn, kn, 1e-6, cs, k1, v1, 1)
+    q = hip.qk_norm_rope_kv_write(qkv, pos, slots, n_q, n_kv, hd, qn, kn, 1e-6, cs, k2, v2, 1)
+    _close(q, q_ref, atol=3e-2)
+    _close(k2, k1, atol=3e-2)
+    _close(v2, v1, atol=0, rtol=0)
+
+
+def _tables(B, lens, NB, max_blocks, gen):
+    perm = torch.randperm(NB - 1, generator=gen) + 1
+    tables = torch.zeros(B, max_blocks, dtype=torch.int32)
+    used = 0
+    for b, n in enumerate(lens):
+        nb = (n + 15) // 16
+        tables[b, :nb] = perm[used:used + nb].to(torch.int32)
+        used += nb
+    return tables.cuda()
+
+
+@pytest.mark.parametrize("n_q,n_kv,hd", [(40, 8, 128), (16, 2, 128), (14, 2, 64)])
+def test_paged_attention_decode(hip, n_q, n_kv, hd):
+    gen = torch.Generator().manual_seed(2)
+    lens = [1, 15, 16, 17, 255, 256, 257, 700, 1500]
+    B, NB, L = len(lens), 256, 2
+    k, v = _caches(L, NB, n_kv, hd)
+    tables = _tables(B, lens, NB, 128, gen)
+    seq = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    q = torch.randn(B, n_q, hd, device="cuda", dtype=torch.bfloat16)
+    scale = hd ** -0.5
+    ref = R.paged_attention(q, k, v, 1, tables, torch.arange(B + 1, dtype=torch.int32, device="cuda"), seq, scale)
+    out = hip.paged_attention_decode(q, k, v, 1, tables, seq, scale)
+    _close(out, ref, atol=2e-2)
+
+
+def _prefill_tiles(q_start, seq_lens):
+    tiles = []
+    for i in range(len(q_start) - 1):
+        for t in range(q_start[i], q_start[i + 1], 64):
+            tiles.append((i, t, min(t + 64, q_start[i + 1])))
+    return torch.tensor(tiles, dtype=torch.int32, device="cuda")
+
+
+@pytest.mark.parametrize("n_q,n_kv,hd", [(40, 8, 128), (14, 2, 64)])
+def test_paged_attention_prefill(hip, n_q, n_kv, hd):
+    gen = torch.Generator().manual_seed(3)
+    # (cached prefix, new tokens)
+    spec = [(0, 1), (0, 37), (16, 50), (32, 64), (0, 300), (160, 129)]
+    ctx = [a + b for a, b in spec]
+    B, NB, L = len(spec), 256, 1
+    k, v = _caches(L, NB, n_kv, hd)
+    tables = _tables(B, ctx, NB, 64, gen)
+    q_start = [0]
+    for _, n in spec:
+        q_start.append(q_start[-1] + n)
+    T = q_start[-1]
+    q = torch.randn(T, n_q, hd, device="cuda", dtype=torch.bfloat16)
+    qs = torch.tensor(q_start, dtype=torch.int32, device="cuda")
+    seq = torch.tensor(ctx, dtype=torch.int32, device="cuda")
+    scale = hd ** -0.5
+    ref = R.paged_attention(q, k, v, 0, tables, qs, seq, scale)
+    out = hip.paged_attention_prefill(q, k, v, 0, tables, qs, seq, scale, max(n for _, n in spec),
+                                      _prefill_tiles(q_start, ctx))
+    _close(out, ref, atol=2e-2)
+
+
+def _sample_state(B, V, rows, base, maxnew, temp, dev="cuda"):
+    return dict(
+        fsm_base=torch.tensor(base, dtype=torch.int32, device=dev),
+        fsm_state=torch.tensor([r % rows for r in range(B)], dtype=torch.int32, device=dev),
+        gen_count=torch.zeros(B, dtype=torch.int32, device=dev),
+        max_new=torch.tensor(maxnew, dtype=torch.int32, device=dev),
+        temperature=torch.tensor(temp, dtype=torch.float32, device=dev),
+        row_keys=torch.arange(B, dtype=torch.int32, device=dev) * 7919 + 3,
+        done=torch.zeros(B, dtype=torch.int32, device=dev),
+        seq_lens=torch.full((B,), 10, dtype=torch.int32, device=dev),
+        out_tokens=torch.zeros(B, 8, dtype=torch.int32, device=dev),
+        next_tokens=torch.zeros(B, dtype=torch.int32, device=dev))
+
+
+@pytest.mark.parametrize("budget", [False, True])
+def test_guided_sample(hip, budget):
+    torch.manual_seed(4)
+    B, V, rows = 12, 151936, 6
+    logits = (torch.randn(B, V, device="cuda") * 3).to(torch.bfloat16)
+    nxt = torch.randint(-1, rows, (rows, V), device="cuda", dtype=torch.int16)
+    nxt[nxt < 2] = -1
+    dist = torch.tensor([5, 4, 3, 2, 1, 0], dtype=torch.int16, device="cuda")
+    base = [0] * (B - 2) + [-1, -1]
+    temp = [0.0, 0.5, 1.0] * (B // 3)
+    s_ref = _sample_state(B, V, rows, base, [8, 2, 1] * (B // 3), temp)
+    s_hip = {k: v.clone() for k, v in s_ref.items()}
+    args = (nxt, dist)
+    R.sample_step(logits, *args, s_ref["fsm_base"], s_ref["fsm_state"], s_ref["gen_count"], s_ref["max_new"],
+                  s_ref["temperature"], s_ref["row_keys"], s_ref["done"], s_ref["seq_lens"], s_ref["out_tokens"],
+                  s_ref["next_tokens"], 1234, budget, 151000, 151645, 151643)
+    hip.sample_step(logits, *args, s_hip["fsm_base"], s_hip["fsm_state"], s_hip["gen_count"], s_hip["max_new"],
+                    s_hip["temperature"], s_hip["row_keys"], s_hip["done"], s_hip["seq_lens"], s_hip["out_tokens"],
+                    s_hip["next_tokens"], 1234, budget, 151000, 151645, 151643)
+    torch.cuda.synchronize()
+    agree = (s_ref["next_tokens"] == s_hip["next_tokens"]).float().mean().item()
+    assert agree >= 0.9, (s_ref["next_tokens"], s_hip["next_tokens"])
+    for key in ("gen_count", "seq_lens"):
+        assert torch.equal(s_ref[key], s_hip[key]), key
+    # every pick must be allowed
+    for b in range(B):
+        tok = int(s_hip["next_tokens"][b])
+        if base[b] >= 0:
+            assert int(nxt[b % rows, tok]) >= 0
