@@ -74,10 +74,11 @@ PRESETS = {
                                               4864, 151936, qkv_bias=True, tie_embeddings=True,
                                               max_position=32768),
     # CPU-test sized variants (same code paths, real tokenizer vocab)
-    "bcg/tiny-qwen3": ModelConfig("bcg/tiny-qwen3", "qwen3", 128, 2, 4, 2, 32, 256, 151936, qk_norm=True),
-    "bcg/tiny-qwen2": ModelConfig("bcg/tiny-qwen2", "qwen2", 128, 2, 4, 2, 32, 256, 151936,
+    # (head_dim 64/128 only: the HIP attention kernels are specialised for those)
+    "bcg/tiny-qwen3": ModelConfig("bcg/tiny-qwen3", "qwen3", 256, 2, 4, 2, 64, 512, 151936, qk_norm=True),
+    "bcg/tiny-qwen2": ModelConfig("bcg/tiny-qwen2", "qwen2", 256, 2, 4, 2, 64, 512, 151936,
                                   qkv_bias=True, tie_embeddings=True),
-    "bcg/tiny-mistral": ModelConfig("bcg/tiny-mistral", "mistral", 128, 2, 4, 2, 32, 256, 32768, rms_eps=1e-5),
+    "bcg/tiny-mistral": ModelConfig("bcg/tiny-mistral", "mistral", 256, 2, 8, 2, 128, 512, 32768, rms_eps=1e-5),
 }
 
 ALIASES = {
