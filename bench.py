@@ -86,6 +86,7 @@ class SimPool:
         errors = []
 
         def work(sim):
+            threading.current_thread()._bcg_participant = True
             try:
                 sim.run_round()
             except BaseException as exc:  # surface thread failures

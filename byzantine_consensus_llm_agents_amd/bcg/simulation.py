@@ -26,6 +26,7 @@ import csv
 import json
 import os
 import random
+import threading
 from datetime import datetime
 from typing import Dict, List, Optional, Tuple
 
@@ -101,6 +102,46 @@ def is_valid_vote(result: Optional[Dict]) -> bool:
     if result is None or "error" in result:
         return False
     return result.get("decision", "") in ["stop", "continue"]
+
+
+def run_concurrently(engine_agent, jobs):
+    """Run independent per-agent retry ladders concurrently (one engine batch per attempt).
+
+    The reference runs them one agent after another (main.py:327-333,
+    :432-437); each ladder only depends on its own agent, so running them in
+    threads whose engine calls the LLM coalesces yields the same per-agent
+    results with one engine call per attempt instead of one per agent.
+    """
+    llm = getattr(engine_agent, "llm", None)
+    if len(jobs) <= 1 or llm is None or not hasattr(llm, "register_client"):
+        return [job() for job in jobs]
+    results = [None] * len(jobs)
+    errors = []
+
+    def work(i, job):
+        try:
+            results[i] = job()
+        except BaseException as exc:
+            errors.append(exc)
+        finally:
+            llm.unregister_client()
+
+    for _ in jobs:
+        llm.register_client()
+    threads = [threading.Thread(target=work, args=(i, j)) for i, j in enumerate(jobs)]
+    for t in threads:
+        t.start()
+    # the calling thread stops counting as a participant while it waits
+    parent = getattr(threading.current_thread(), "_bcg_participant", False)
+    if parent:
+        llm.unregister_client()
+    for t in threads:
+        t.join()
+    if parent:
+        llm.register_client()
+    if errors:
+        raise errors[0]
+    return results
 
 
 def topology_for(num_agents: int) -> NetworkTopology:
@@ -192,6 +233,9 @@ class BCGSimulation:
         self.log(f"All agents created! Total: {len(self.agents)}")
         self.log("=" * 60 + "\n")
 
+    def _engine_agent(self):
+        return next(iter(self.agents.values()))
+
     def _is_valid_decision_response(self, result: Dict) -> bool:
         return is_valid_decision(result)
 
@@ -243,10 +287,11 @@ class BCGSimulation:
             return
 
         def sequential(pending, results):
+            self.counters["sequential_calls"] += len(pending)
+            values = run_concurrently(self._engine_agent(), [
+                (lambda a=self.agents[aid]: a.decide_next_value(game_state)) for aid, _ in pending])
             still = []
-            for aid, prompt in pending:
-                self.counters["sequential_calls"] += 1
-                value = self.agents[aid].decide_next_value(game_state)
+            for (aid, prompt), value in zip(pending, values):
                 if value is not None:
                     results[aid] = {"_sequential_success": True, "value": value}
                 else:
@@ -282,10 +327,11 @@ class BCGSimulation:
         jobs = [(aid, agent.build_vote_prompt(game_state)) for aid, agent in self.agents.items()]
 
         def sequential(pending, results):
-            for aid, _ in pending:
-                self.counters["sequential_calls"] += 1
-                results[aid] = {"_sequential_success": True,
-                                "vote": self.agents[aid].vote_to_terminate(game_state)}
+            self.counters["sequential_calls"] += len(pending)
+            votes = run_concurrently(self._engine_agent(), [
+                (lambda a=self.agents[aid]: a.vote_to_terminate(game_state)) for aid, _ in pending])
+            for (aid, _), vote in zip(pending, votes):
+                results[aid] = {"_sequential_success": True, "vote": vote}
             return []
 
         results = self._ladder(jobs, LLM_CONFIG["temperature_vote"], LLM_CONFIG["max_tokens_vote"],

@@ -181,6 +181,15 @@ class InferenceEngine:
 
     # ------------------------------------------------------------ serving
     def generate(self, prompts: List[str], params_list) -> List[str]:
+        # the coalescer may run this on any simulation thread; the current HIP
+        # device (and with it torch.cuda.current_stream used by the ctypes
+        # launches) is thread-local, so pin it for the whole call
+        if self.device.type == "cuda":
+            with torch.cuda.device(self.device):
+                return self._generate(prompts, params_list)
+        return self._generate(prompts, params_list)
+
+    def _generate(self, prompts: List[str], params_list) -> List[str]:
         self.stats["calls"] += 1
         with self.timer.phase("tokenize"):
             ids = self.tokenizer.encode_batch(prompts)

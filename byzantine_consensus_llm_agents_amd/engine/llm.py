@@ -151,15 +151,15 @@ class LLM:
             self.backend = InferenceEngine(args)
         else:
             raise ValueError(f"unknown engine backend {self.backend_name!r}")
+        # every call goes through the coalescer: with no registered clients it
+        # flushes immediately, with N registered threads it waits for all of them
         self.coalescer = Coalescer(self._run_batch)
-        self._coalesce = False
         self._next_id = 0
         self.stats = {"calls": 0, "sequences": 0, "seconds": 0.0}
 
     # --------------------------------------------------- multi-sim sharing
     def register_client(self):
-        """Declare one more simulation thread whose calls should be coalesced."""
-        self._coalesce = True
+        """Declare one more thread whose calls should be coalesced with the others'."""
         self.coalescer.join()
 
     def unregister_client(self):
@@ -190,10 +190,7 @@ class LLM:
                 raise ValueError("need one SamplingParams per prompt")
         if not prompts:
             return []
-        if self._coalesce:
-            texts = self.coalescer.submit(prompts, params)
-        else:
-            texts = self._run_batch(prompts, params)
+        texts = self.coalescer.submit(prompts, params)
         outs = []
         for p, t in zip(prompts, texts):
             outs.append(RequestOutput(self._next_id, p, [CompletionOutput(0, t)]))
