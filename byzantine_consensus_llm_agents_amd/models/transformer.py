@@ -186,7 +186,7 @@ class DecoderModel:
         residual = None
         for li, L in enumerate(self.layers):
             h, residual = ops.add_rmsnorm(x, residual, L["ln1"], c.rms_eps)
-            qkv = F.linear(h, L["qkv"], L.get("qkv_bias"))
+            qkv = ops.linear(h, L["qkv"], L.get("qkv_bias"))
             q = ops.qk_norm_rope_kv_write(qkv, meta.positions, meta.slots, self.n_q, self.n_kv, self.hd,
                                           L.get("q_norm"), L.get("k_norm"), c.rms_eps, self.cos_sin,
                                           k_cache, v_cache, li)
@@ -197,13 +197,13 @@ class DecoderModel:
                 attn = ops.paged_attention_prefill(q, k_cache, v_cache, li, meta.block_tables,
                                                    meta.q_start, meta.seq_lens, self.scale, meta.max_q_len,
                                                    meta.tiles)
-            x = self.tp.all_reduce_(F.linear(attn, L["o"]))
+            x = self.tp.all_reduce_(ops.linear(attn, L["o"]))
             h, residual = ops.add_rmsnorm(x, residual, L["ln2"], c.rms_eps)
-            gu = F.linear(h, L["gate_up"])
-            x = self.tp.all_reduce_(F.linear(ops.silu_mul(gu), L["down"]))
+            gu = ops.linear(h, L["gate_up"])
+            x = self.tp.all_reduce_(ops.linear(ops.silu_mul(gu), L["down"]))
         if meta.logits_idx is not None:
             x = x.index_select(0, meta.logits_idx)
             residual = residual.index_select(0, meta.logits_idx)
         h, _ = ops.add_rmsnorm(x, residual, self.final_norm, c.rms_eps)
-        logits = F.linear(h, self.lm_head)
+        logits = ops.linear(h, self.lm_head)
         return self.tp.all_gather_last(logits)

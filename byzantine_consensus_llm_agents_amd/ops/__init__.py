@@ -23,6 +23,7 @@ def _torch_ops() -> SimpleNamespace:
 
     return SimpleNamespace(
         name="torch",
+        linear=torch.nn.functional.linear,
         rmsnorm=_ref.rmsnorm,
         add_rmsnorm=_ref.add_rmsnorm,
         qk_norm_rope_kv_write=_ref.qk_norm_rope_kv_write,

@@ -41,6 +41,9 @@ def load_library(path: str = None) -> ctypes.CDLL:
         "bcg_paged_attention_prefill": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                                         c_void_p, c_void_p],
+        "bcg_decode_split_tokens": [],
+        "bcg_gemm_skinny": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                            c_void_p],
         "bcg_guided_sample": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                               c_uint32, c_int, c_int, c_int, c_int, c_void_p],
@@ -73,7 +76,7 @@ def _req(cond: bool, msg: str):
 
 def hip_ops() -> SimpleNamespace:
     lib = load_library()
-    SPLIT = 256
+    SPLIT = lib.bcg_decode_split_tokens()
 
     def add_rmsnorm(x, residual, w, eps):
         _req(x.dtype == torch.bfloat16 and x.is_contiguous() and x.dim() == 2, "add_rmsnorm: x bf16 [T,H]")
@@ -145,6 +148,30 @@ def hip_ops() -> SimpleNamespace:
             "paged_attention_prefill")
         return out
 
+    use_skinny = os.environ.get("BCG_SKINNY_GEMM", "1") != "0"
+    skinny_max_m = int(os.environ.get("BCG_SKINNY_MAX_M", "192"))
+
+    def skinny_split(N: int, K: int) -> int:
+        nblocks = N // 128
+        ksteps = K // 32
+        # aim for ~2 workgroups per CU, keep >= 8 k-steps (256 of K) per split
+        return max(1, min(512 // nblocks, ksteps // 8))
+
+    def linear(x, w, bias=None):
+        """y = x W^T (+b): MFMA weight-streaming kernel for decode shapes, hipBLASLt otherwise."""
+        M, K = x.shape
+        N = w.shape[0]
+        if not (use_skinny and M <= skinny_max_m and N % 128 == 0 and K % 128 == 0 and x.is_contiguous()
+                and w.is_contiguous() and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
+            return torch.nn.functional.linear(x, w, bias)
+        _req(w.shape[1] == K and (bias is None or bias.shape == (N,)), "linear shapes")
+        split = skinny_split(N, K)
+        y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+        ws = torch.zeros(M, N, dtype=torch.float32, device=x.device) if split > 1 else None
+        _check(lib.bcg_gemm_skinny(_p(x), _p(w), _p(bias) if bias is not None else None, _p(y),
+                                   _p(ws) if ws is not None else None, M, N, K, split, _stream()), "gemm_skinny")
+        return y
+
     def sample_step(logits, fsm_next, fsm_dist, fsm_base, fsm_state, gen_count, max_new, temperature,
                     row_keys, done, seq_lens, out_tokens, next_tokens, seed, budget_aware, n_text_tokens,
                     eos_id, eos_id2):
@@ -162,7 +189,7 @@ def hip_ops() -> SimpleNamespace:
             out_tokens.shape[1], _p(next_tokens), seed & 0xFFFFFFFF, int(bool(budget_aware)), n_text_tokens,
             eos_id, eos_id2, _stream()), "guided_sample")
 
-    return SimpleNamespace(name="hip", rmsnorm=rmsnorm, add_rmsnorm=add_rmsnorm, silu_mul=silu_mul,
+    return SimpleNamespace(name="hip", linear=linear, rmsnorm=rmsnorm, add_rmsnorm=add_rmsnorm, silu_mul=silu_mul,
                            qk_norm_rope_kv_write=qk_norm_rope_kv_write,
                            paged_attention_decode=paged_attention_decode,
                            paged_attention_prefill=paged_attention_prefill, sample_step=sample_step,

@@ -6,29 +6,34 @@
 //   O^T += V^T · P^T   A = V^T read from the *transposed* V cache ([hd][BS] per
 //                      block-head), B = P^T built lane-locally from the S^T
 //                      accumulators (no LDS, no shuffles).
-// With this orientation every per-query quantity (running max m, sum l, the
-// rescale factor, the O^T columns) lives on lane column q = lane & 15, so the
-// online softmax needs only two xor-shuffles per chunk and no data movement
-// between the two MFMAs.
+// Every per-query quantity (running max m, sum l, rescale factor, O^T column)
+// lives on lane column q = lane & 15: the online softmax needs two
+// xor-shuffles per 32-token chunk and no data movement between the MFMAs.
 //
 // MFMA 16x16x32 bf16 lane maps (gfx950):
 //   A[row = l&15][k = 8(l>>4)+j], B[k = 8(l>>4)+j][col = l&15], C[row = 4(l>>4)+i][col = l&15]
-// K-slot permutation used for P/V (same on both operands, so the sum is exact):
-//   slot (h, j<4) -> token 4h+j of block 0 of the chunk, (h, j>=4) -> token 4h+j-4 of block 1.
+// Token permutation of a 32-token chunk (makes every V fragment ONE 16-byte load):
+//   S^T tile u (u = 0,1), C row 4h+i  <->  chunk token 8h + 4u + i
+//   so lane group h holds the scores of tokens 8h..8h+7, which is exactly the
+//   k-slot order (h, j) <-> token 8h+j of the P^T / V^T operands; tokens 8h..8h+7
+//   are 16 contiguous bytes of one V^T row (block h>>1, offset 8(h&1)).
+//   K tiles load row r from token 8(r>>2) + 4u + (r&3) (a row gather: free).
 //
-// Decode: one workgroup per (sequence, kv head, 256-token split); the G = n_q/n_kv
+// Decode: one workgroup per (sequence, kv head, 512-token split); the G = n_q/n_kv
 // query heads of the kv head share every K/V byte (GQA packing: 5 for Qwen3-14B).
-// 4 waves x 64 tokens, combined through LDS; splits merged by a second kernel
-// (flash-decoding).  Prefill: one workgroup per (64-query tile, query head),
-// causal over the cached prefix + the new tokens, varlen via a tile table.
+// 4 waves x 128 tokens with the next chunk's K/V loads in flight while the
+// current chunk computes; waves combined through LDS, splits merged by a second
+// kernel (flash-decoding).  Prefill: one workgroup per (64-query tile, query
+// head), causal over cached prefix + new tokens, varlen via a tile table.
 
 #include "common.h"
 
 namespace {
 
 constexpr int BS = 16;            // KV block size (tokens)
-constexpr int SPLIT = 256;        // decode tokens per workgroup
+constexpr int SPLIT = 512;        // decode tokens per workgroup
 constexpr int DEC_WAVES = 4;
+constexpr int CHUNK = 32;
 constexpr float LOG2E = 1.4426950408889634f;
 
 struct KVGeom {
@@ -42,41 +47,65 @@ __device__ __forceinline__ size_t block_base(const KVGeom& g, int blk, int kvh) 
   return ((static_cast<size_t>(g.layer) * g.num_blocks + blk) * g.n_kv + kvh) * (BS * HD);
 }
 
-// S^T for one 16-token block: returns C (rows = token 4h+i, col = q).
 template <int HD>
-__device__ __forceinline__ f32x4 qk_block(const bf16_t* kblock, const bf16x8 (&bq)[HD / 32], int lane) {
+struct Chunk {
+  bf16x8 k[2][HD / 32];   // S^T A-operands, tile u, k-step kk
+  bf16x8 v[HD / 16];      // O^T A-operands, d-tile dt
+};
+
+// Issue every load of one 32-token chunk whose blocks are blk0/blk1.
+template <int HD>
+__device__ __forceinline__ void load_chunk(Chunk<HD>& c, const KVGeom& g, int blk0, int blk1, int kvh, int lane) {
   const int r = lane & 15, h = lane >> 4;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const size_t b0 = block_base<HD>(g, blk0, kvh), b1 = block_base<HD>(g, blk1, kvh);
 #pragma unroll
-  for (int kk = 0; kk < HD / 32; ++kk) {
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(kblock + r * HD + kk * 32 + h * 8);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[kk], acc, 0, 0, 0);
+  for (int u = 0; u < 2; ++u) {
+    const int t = 8 * (r >> 2) + 4 * u + (r & 3);
+    const bf16_t* krow = g.k + (t < BS ? b0 : b1) + (t & (BS - 1)) * HD + 8 * h;
+#pragma unroll
+    for (int kk = 0; kk < HD / 32; ++kk) c.k[u][kk] = *reinterpret_cast<const bf16x8*>(krow + kk * 32);
   }
-  return acc;
+  const bf16_t* vb = g.v + (h < 2 ? b0 : b1) + 8 * (h & 1);
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt) c.v[dt] = *reinterpret_cast<const bf16x8*>(vb + (dt * 16 + r) * BS);
 }
 
-// One 32-token chunk: online-softmax update + O^T accumulation.
-// s0/s1: raw scores of tokens (4h+i) of block 0/1, already scaled to log2 units and masked.
-template <int HD>
-__device__ __forceinline__ void softmax_pv(f32x4 s0, f32x4 s1, const bf16_t* vb0, const bf16_t* vb1,
-                                           bool v0_ok[4], bool v1_ok[4], float& m, float& l,
-                                           f32x4 (&o)[HD / 16], int lane) {
-  const int r = lane & 15, h = lane >> 4;
-  float mx = fmaxf(fmaxf(fmaxf(s0[0], s0[1]), fmaxf(s0[2], s0[3])), fmaxf(fmaxf(s1[0], s1[1]), fmaxf(s1[2], s1[3])));
+// Online-softmax update + O^T accumulation for one chunk starting at token t0.
+// visible(t) decides masking (t = absolute token index); n_valid bounds V reads.
+template <int HD, typename Vis>
+__device__ __forceinline__ void compute_chunk(const Chunk<HD>& c, const bf16x8 (&bq)[HD / 32], int t0, int kv_end,
+                                              Vis visible, float scale_log2, float& m, float& l,
+                                              f32x4 (&o)[HD / 16], int lane) {
+  const int h = lane >> 4;
+  f32x4 s[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    s[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < HD / 32; ++kk)
+      s[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.k[u][kk], bq[kk], s[u], 0, 0, 0);
+  }
+  float p[8];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int t = t0 + 8 * h + j;
+    const float sv = s[j >> 2][j & 3];
+    p[j] = (t < kv_end && visible(t)) ? sv * scale_log2 : -INFINITY;
+    mx = fmaxf(mx, p[j]);
+  }
   mx = fmaxf(mx, __shfl_xor(mx, 16, WAVE));
   mx = fmaxf(mx, __shfl_xor(mx, 32, WAVE));
   // no early exit: the MFMAs below must run with every lane active
   const float m_new = fmaxf(m, mx);
-  const bool any = m_new != -INFINITY;
-  const float m_use = any ? m_new : 0.f;
-  const float alpha = (m == -INFINITY) ? 0.f : exp2f(m - m_use);
-  float p[8];
+  const float m_use = m_new == -INFINITY ? 0.f : m_new;
+  const float alpha = m == -INFINITY ? 0.f : exp2f(m - m_use);
+  float ps = 0.f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    p[i] = exp2f(s0[i] - m_use);
-    p[4 + i] = exp2f(s1[i] - m_use);
+  for (int j = 0; j < 8; ++j) {
+    p[j] = exp2f(p[j] - m_use);
+    ps += p[j];
   }
-  float ps = ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
   ps += __shfl_xor(ps, 16, WAVE);
   ps += __shfl_xor(ps, 32, WAVE);
   l = l * alpha + ps;
@@ -84,21 +113,40 @@ __device__ __forceinline__ void softmax_pv(f32x4 s0, f32x4 s1, const bf16_t* vb0
   bf16x8 bp;
 #pragma unroll
   for (int j = 0; j < 8; ++j) bp[j] = static_cast<__bf16>(p[j]);
+  // tokens past kv_end may hold stale (even non-finite) bytes: zero their V
+  const bool v_ok = t0 + 8 * h + 7 < kv_end;
 #pragma unroll
   for (int dt = 0; dt < HD / 16; ++dt) {
     o[dt] *= alpha;
-    const int d = dt * 16 + r;
-    u16x4 lo = *reinterpret_cast<const u16x4*>(vb0 + d * BS + 4 * h);
-    u16x4 hi = *reinterpret_cast<const u16x4*>(vb1 + d * BS + 4 * h);
-    u16x8 av;
+    bf16x8 va = c.v[dt];
+    if (!v_ok) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      av[i] = v0_ok[i] ? lo[i] : static_cast<uint16_t>(0);
-      av[4 + i] = v1_ok[i] ? hi[i] : static_cast<uint16_t>(0);
+      for (int j = 0; j < 8; ++j)
+        if (t0 + 8 * h + j >= kv_end) va[j] = static_cast<__bf16>(0.f);
     }
-    o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av), bp, o[dt], 0, 0, 0);
+    o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, bp, o[dt], 0, 0, 0);
   }
 }
+
+template <int HD>
+__device__ __forceinline__ void load_q(bf16x8 (&bq)[HD / 32], const bf16_t* row, bool ok, int lane) {
+  const int h = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < HD / 32; ++kk) {
+    u16x8 v = *reinterpret_cast<const u16x8*>(row + kk * 32 + h * 8);
+    if (!ok) v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    bq[kk] = __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+struct AllVisible {
+  __device__ bool operator()(int) const { return true; }
+};
+
+struct Causal {
+  int pos;
+  __device__ bool operator()(int t) const { return t <= pos; }
+};
 
 // ------------------------------------------------------------------ decode
 template <int HD>
@@ -115,45 +163,40 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   const int G = n_q / g.n_kv;
   const int* table = block_tables + static_cast<size_t>(b) * max_blocks;
 
-  // Q^T fragment: col = query head (kvh*G + r), k = dims.
   bf16x8 bq[HD / 32];
-  const bool q_ok = r < G;
-  const bf16_t* qrow = q + (static_cast<size_t>(b) * n_q + kvh * G + (q_ok ? r : 0)) * HD;
-#pragma unroll
-  for (int kk = 0; kk < HD / 32; ++kk) {
-    u16x8 v = *reinterpret_cast<const u16x8*>(qrow + kk * 32 + h * 8);
-    if (!q_ok) v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    bq[kk] = __builtin_bit_cast(bf16x8, v);
-  }
+  load_q<HD>(bq, q + (static_cast<size_t>(b) * n_q + kvh * G + (r < G ? r : 0)) * HD, r < G, lane);
 
   float m = -INFINITY, l = 0.f;
   f32x4 o[HD / 16];
 #pragma unroll
   for (int dt = 0; dt < HD / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int t0 = start + w * 64 + c * 32;
-    if (t0 >= ctx) break;
-    const int blk0 = table[t0 / BS];
-    const int blk1 = (t0 + BS < ctx) ? table[t0 / BS + 1] : blk0;
-    const size_t base0 = block_base<HD>(g, blk0, kvh), base1 = block_base<HD>(g, blk1, kvh);
-    f32x4 s0 = qk_block<HD>(g.k + base0, bq, lane);
-    f32x4 s1 = qk_block<HD>(g.k + base1, bq, lane);
-    bool ok0[4], ok1[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      ok0[i] = t0 + 4 * h + i < ctx;
-      ok1[i] = t0 + BS + 4 * h + i < ctx;
-      s0[i] = ok0[i] ? s0[i] * scale_log2 : -INFINITY;
-      s1[i] = ok1[i] ? s1[i] * scale_log2 : -INFINITY;
+  constexpr int PER_WAVE = SPLIT / DEC_WAVES;  // 128 tokens = 4 chunks
+  const int wbeg = start + w * PER_WAVE;
+  const int wend = min(ctx, wbeg + PER_WAVE);
+  if (wbeg < wend) {
+    auto blocks_of = [&](int t0, int& b0, int& b1) {
+      b0 = table[t0 / BS];
+      b1 = (t0 + BS < ctx) ? table[t0 / BS + 1] : b0;
+    };
+    Chunk<HD> cur, nxt;
+    int b0, b1;
+    blocks_of(wbeg, b0, b1);
+    load_chunk<HD>(cur, g, b0, b1, kvh, lane);
+    for (int t0 = wbeg; t0 < wend; t0 += CHUNK) {
+      const bool more = t0 + CHUNK < wend;
+      if (more) {
+        blocks_of(t0 + CHUNK, b0, b1);
+        load_chunk<HD>(nxt, g, b0, b1, kvh, lane);
+      }
+      compute_chunk<HD>(cur, bq, t0, ctx, AllVisible{}, scale_log2, m, l, o, lane);
+      if (more) cur = nxt;
     }
-    softmax_pv<HD>(s0, s1, g.v + base0, g.v + base1, ok0, ok1, m, l, o, lane);
   }
 
   // combine the 4 waves through LDS
   __shared__ float s_ml[DEC_WAVES][2][16];
-  __shared__ float s_o[DEC_WAVES][HD][16];
+  __shared__ float s_o[DEC_WAVES][HD][16 + 1];
   if (h == 0) {
     s_ml[w][0][r] = m;
     s_ml[w][1][r] = l;
@@ -230,37 +273,31 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   const bool row_ok = my_row < q_end;
   const int my_pos = pos0 + (my_row - qs);
   const int last_row = min(row0 + 15, q_end - 1);
-  const int kv_end = pos0 + (last_row - qs) + 1;  // exclusive bound of visible keys for this wave
+  const int kv_end = pos0 + (last_row - qs) + 1;  // exclusive bound of keys visible to this wave
 
   bf16x8 bq[HD / 32];
-  const bf16_t* qrow = q + (static_cast<size_t>(row_ok ? my_row : row0) * n_q + qh) * HD;
-#pragma unroll
-  for (int kk = 0; kk < HD / 32; ++kk) {
-    u16x8 v = *reinterpret_cast<const u16x8*>(qrow + kk * 32 + h * 8);
-    if (!row_ok) v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    bq[kk] = __builtin_bit_cast(bf16x8, v);
-  }
+  load_q<HD>(bq, q + (static_cast<size_t>(row_ok ? my_row : row0) * n_q + qh) * HD, row_ok, lane);
   float m = -INFINITY, l = 0.f;
   f32x4 o[HD / 16];
 #pragma unroll
   for (int dt = 0; dt < HD / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int t0 = 0; t0 < kv_end; t0 += 32) {
-    const int blk0 = table[t0 / BS];
-    const int blk1 = (t0 + BS < kv_end) ? table[t0 / BS + 1] : blk0;
-    const size_t base0 = block_base<HD>(g, blk0, kvh), base1 = block_base<HD>(g, blk1, kvh);
-    f32x4 s0 = qk_block<HD>(g.k + base0, bq, lane);
-    f32x4 s1 = qk_block<HD>(g.k + base1, bq, lane);
-    bool ok0[4], ok1[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ta = t0 + 4 * h + i, tb = t0 + BS + 4 * h + i;
-      ok0[i] = ta < kv_end;
-      ok1[i] = tb < kv_end;
-      s0[i] = (ok0[i] && ta <= my_pos) ? s0[i] * scale_log2 : -INFINITY;
-      s1[i] = (ok1[i] && tb <= my_pos) ? s1[i] * scale_log2 : -INFINITY;
+  auto blocks_of = [&](int t0, int& b0, int& b1) {
+    b0 = table[t0 / BS];
+    b1 = (t0 + BS < kv_end) ? table[t0 / BS + 1] : b0;
+  };
+  Chunk<HD> cur, nxt;
+  int b0, b1;
+  blocks_of(0, b0, b1);
+  load_chunk<HD>(cur, g, b0, b1, kvh, lane);
+  for (int t0 = 0; t0 < kv_end; t0 += CHUNK) {
+    const bool more = t0 + CHUNK < kv_end;
+    if (more) {
+      blocks_of(t0 + CHUNK, b0, b1);
+      load_chunk<HD>(nxt, g, b0, b1, kvh, lane);
     }
-    softmax_pv<HD>(s0, s1, g.v + base0, g.v + base1, ok0, ok1, m, l, o, lane);
+    compute_chunk<HD>(cur, bq, t0, kv_end, Causal{my_pos}, scale_log2, m, l, o, lane);
+    if (more) cur = nxt;
   }
   if (!row_ok) return;
   const float inv = l > 0.f ? 1.f / l : 0.f;
@@ -277,9 +314,7 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
 
 }  // namespace
 
-BCG_API int bcg_decode_workspace_floats(int B, int n_q, int hd, int max_splits) {
-  return B * n_q * max_splits * (hd + 2);
-}
+BCG_API int bcg_decode_split_tokens() { return SPLIT; }
 
 BCG_API int bcg_paged_attention_decode(const void* q, const void* k_cache, const void* v_cache, int layer,
                                        int num_blocks, int n_kv, const int* block_tables, int max_blocks,
@@ -287,6 +322,7 @@ BCG_API int bcg_paged_attention_decode(const void* q, const void* k_cache, const
                                        float scale, float* workspace, int max_splits, void* out,
                                        hipStream_t stream) {
   if (block_size != BS || n_q % n_kv || n_q / n_kv > 16 || B <= 0) return -2;
+  if (max_splits * SPLIT < max_blocks * BS) return -3;
   KVGeom g{static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), layer, num_blocks, n_kv};
   float* part_o = workspace;
   float* part_ml = workspace + static_cast<size_t>(B) * n_q * max_splits * hd;

@@ -163,3 +163,15 @@ def test_guided_sample(hip, budget):
         tok = int(s_hip["next_tokens"][b])
         if base[b] >= 0:
             assert int(nxt[b % rows, tok]) >= 0
+
+
+@pytest.mark.parametrize("M,N,K,bias", [(1, 5120, 5120, False), (40, 34816, 5120, False), (37, 5120, 17408, False),
+                                        (128, 7168, 5120, True), (160, 5120, 5120, False), (192, 34816, 5120, False), (70, 1152, 896, True), (16, 151936, 5120, False)])
+def test_gemm_skinny(hip, M, N, K, bias):
+    torch.manual_seed(5)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16) if bias else None
+    ref = torch.nn.functional.linear(x.float(), w.float(), None if b is None else b.float())
+    out = hip.linear(x, w, b)
+    _close(out, ref, atol=2e-2, rtol=2e-2)

@@ -1,0 +1,103 @@
+"""Micro-benchmarks of the decode hot ops on one MI355X (interleaved A/B in one process).
+
+  python tools/bench_ops.py [--model qwen3-14b] [--ms 16,40,80,128,160,192]
+
+Reports per-op time and effective HBM bandwidth (weight / KV bytes moved) for:
+  * decode projections: MFMA skinny GEMM vs torch.nn.functional.linear (hipBLASLt);
+  * paged decode attention (bytes = K+V of every context token);
+  * the fused guided sampler.
+Writes a JSON summary to gpurun_out/bench_ops.json.
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from byzantine_consensus_llm_agents_amd.models.config import get_model_config  # noqa: E402
+from byzantine_consensus_llm_agents_amd.ops import get_ops  # noqa: E402
+
+
+def timeit(fn, iters=20, warmup=3):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    start.record()
+    for _ in range(iters):
+        fn()
+    end.record()
+    torch.cuda.synchronize()
+    return start.elapsed_time(end) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="qwen3-14b")
+    ap.add_argument("--ms", default="16,40,80,128,160,192")
+    ap.add_argument("--ctx", type=int, default=1700)
+    args = ap.parse_args()
+    hip = get_ops("hip")
+    cfg = get_model_config(args.model)
+    H, I, hd = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim
+    shapes = {"qkv": ((cfg.num_heads + 2 * cfg.num_kv_heads) * hd, H), "o": (H, cfg.num_heads * hd),
+              "gate_up": (2 * I, H), "down": (H, I), "lm_head": (cfg.vocab_size, H)}
+    weights = {k: torch.randn(n, kk, device="cuda", dtype=torch.bfloat16) * 0.02 for k, (n, kk) in shapes.items()}
+    out = {"model": cfg.name, "gemm": [], "attention": [], "sample": []}
+    for M in [int(m) for m in args.ms.split(",")]:
+        x = {k: torch.randn(M, kk, device="cuda", dtype=torch.bfloat16) for k, (n, kk) in shapes.items()}
+        for name, w in weights.items():
+            t_sk = timeit(lambda: hip.linear(x[name], w))
+            t_bl = timeit(lambda: torch.nn.functional.linear(x[name], w))
+            gb = w.numel() * 2 / 1e9
+            rec = {"M": M, "op": name, "skinny_us": round(t_sk, 1), "hipblaslt_us": round(t_bl, 1),
+                   "skinny_TBps": round(gb / t_sk * 1e3, 2), "hipblaslt_TBps": round(gb / t_bl * 1e3, 2)}
+            out["gemm"].append(rec)
+            print(json.dumps(rec), flush=True)
+    # decode attention at the bench geometry
+    NB = 1 + (args.ctx // 16 + 1) * 192
+    k = torch.randn(1, NB, cfg.num_kv_heads, 16, hd, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(1, NB, cfg.num_kv_heads, hd, 16, device="cuda", dtype=torch.bfloat16)
+    for B in (40, 160, 192):
+        nb = (args.ctx + 15) // 16
+        tables = (torch.arange(B * nb, dtype=torch.int32, device="cuda").view(B, nb) + 1)
+        tables = torch.cat([tables, torch.zeros(B, 512 - nb, dtype=torch.int32, device="cuda")], 1).contiguous()
+        seq = torch.full((B,), args.ctx, dtype=torch.int32, device="cuda")
+        q = torch.randn(B, cfg.num_heads, hd, device="cuda", dtype=torch.bfloat16)
+        t = timeit(lambda: hip.paged_attention_decode(q, k, v, 0, tables, seq, hd ** -0.5))
+        gb = B * args.ctx * cfg.num_kv_heads * hd * 2 * 2 / 1e9
+        rec = {"B": B, "ctx": args.ctx, "us": round(t, 1), "TBps": round(gb / t * 1e3, 2)}
+        out["attention"].append(rec)
+        print(json.dumps(rec), flush=True)
+    # sampler
+    V = cfg.vocab_size
+    for B in (40, 160):
+        logits = torch.randn(B, V, device="cuda", dtype=torch.bfloat16)
+        nxt = torch.randint(-1, 100, (128, V), device="cuda", dtype=torch.int16)
+        dist = torch.randint(0, 50, (128,), device="cuda", dtype=torch.int16)
+        st = {n: torch.zeros(B, dtype=torch.int32, device="cuda") for n in
+              ("fsm_base", "fsm_state", "gen_count", "row_keys", "done", "seq_lens", "next_tokens")}
+        mx = torch.full((B,), 1 << 30, dtype=torch.int32, device="cuda")
+        temp = torch.full((B,), 0.5, device="cuda")
+        outt = torch.zeros(B, 1 << 14, dtype=torch.int32, device="cuda")
+
+        def run():
+            st["gen_count"].zero_()
+            hip.sample_step(logits, nxt, dist, st["fsm_base"], st["fsm_state"], st["gen_count"], mx, temp,
+                            st["row_keys"], st["done"], st["seq_lens"], outt, st["next_tokens"], 7, True,
+                            V - 500, 0, 1)
+        t = timeit(run)
+        rec = {"B": B, "V": V, "us": round(t, 1)}
+        out["sample"].append(rec)
+        print(json.dumps(rec), flush=True)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "bench_ops.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
