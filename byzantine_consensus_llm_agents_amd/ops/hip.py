@@ -148,7 +148,7 @@ def hip_ops() -> SimpleNamespace:
             "paged_attention_prefill")
         return out
 
-    use_skinny = os.environ.get("BCG_SKINNY_GEMM", "1") != "0"
+    use_skinny = os.environ.get("BCG_SKINNY_GEMM", "0") == "1"  # hipBLASLt wins (bench_ops r1)
     skinny_max_m = int(os.environ.get("BCG_SKINNY_MAX_M", "192"))
 
     def skinny_split(N: int, K: int) -> int:

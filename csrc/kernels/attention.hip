@@ -171,22 +171,29 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
 #pragma unroll
   for (int dt = 0; dt < HD / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  constexpr int PER_WAVE = SPLIT / DEC_WAVES;  // 128 tokens = 4 chunks
+  constexpr int PER_WAVE = SPLIT / DEC_WAVES;  // 128 tokens = 4 chunks = 8 blocks
   const int wbeg = start + w * PER_WAVE;
   const int wend = min(ctx, wbeg + PER_WAVE);
   if (wbeg < wend) {
-    auto blocks_of = [&](int t0, int& b0, int& b1) {
-      b0 = table[t0 / BS];
-      b1 = (t0 + BS < ctx) ? table[t0 / BS + 1] : b0;
-    };
+    // Block ids of this wave's 8 blocks: one load per lane up front, then broadcast
+    // with readlane -- a table load inside the chunk loop would sit behind the
+    // previous chunk's K/V loads on the in-order vmcnt counter and serialise it.
+    const int nblk = (wend - wbeg + BS - 1) / BS;
+    const int my_blk = lane < nblk ? table[wbeg / BS + lane] : 0;
     Chunk<HD> cur, nxt;
-    int b0, b1;
-    blocks_of(wbeg, b0, b1);
-    load_chunk<HD>(cur, g, b0, b1, kvh, lane);
-    for (int t0 = wbeg; t0 < wend; t0 += CHUNK) {
+    {
+      const int b0 = __builtin_amdgcn_readlane(my_blk, 0);
+      const int b1 = nblk > 1 ? __builtin_amdgcn_readlane(my_blk, 1) : b0;
+      load_chunk<HD>(cur, g, b0, b1, kvh, lane);
+    }
+#pragma unroll
+    for (int c = 0; c < PER_WAVE / CHUNK; ++c) {
+      const int t0 = wbeg + c * CHUNK;
+      if (t0 >= wend) break;
       const bool more = t0 + CHUNK < wend;
       if (more) {
-        blocks_of(t0 + CHUNK, b0, b1);
+        const int b0 = __builtin_amdgcn_readlane(my_blk, 2 * c + 2);
+        const int b1 = 2 * c + 3 < nblk ? __builtin_amdgcn_readlane(my_blk, 2 * c + 3) : b0;
         load_chunk<HD>(nxt, g, b0, b1, kvh, lane);
       }
       compute_chunk<HD>(cur, bq, t0, ctx, AllVisible{}, scale_log2, m, l, o, lane);
@@ -282,18 +289,29 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
 #pragma unroll
   for (int dt = 0; dt < HD / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto blocks_of = [&](int t0, int& b0, int& b1) {
-    b0 = table[t0 / BS];
-    b1 = (t0 + BS < kv_end) ? table[t0 / BS + 1] : b0;
+  // block ids in windows of 64 (one per lane), broadcast with readlane (see decode)
+  const int nblk = (kv_end + BS - 1) / BS;
+  int win_base = 0;
+  int my_blk = lane < nblk ? table[lane] : 0;
+  auto block_at = [&](int bi) -> int {
+    if (bi >= win_base + 64) {  // wave-uniform: advance the window
+      win_base += 64;
+      my_blk = win_base + lane < nblk ? table[win_base + lane] : 0;
+    }
+    return __builtin_amdgcn_readlane(my_blk, bi - win_base);
   };
   Chunk<HD> cur, nxt;
-  int b0, b1;
-  blocks_of(0, b0, b1);
-  load_chunk<HD>(cur, g, b0, b1, kvh, lane);
+  {
+    const int b0 = block_at(0);
+    const int b1 = nblk > 1 ? block_at(1) : b0;
+    load_chunk<HD>(cur, g, b0, b1, kvh, lane);
+  }
   for (int t0 = 0; t0 < kv_end; t0 += CHUNK) {
     const bool more = t0 + CHUNK < kv_end;
     if (more) {
-      blocks_of(t0 + CHUNK, b0, b1);
+      const int bi = (t0 + CHUNK) / BS;
+      const int b0 = block_at(bi);
+      const int b1 = bi + 1 < nblk ? block_at(bi + 1) : b0;
       load_chunk<HD>(nxt, g, b0, b1, kvh, lane);
     }
     compute_chunk<HD>(cur, bq, t0, kv_end, Causal{my_pos}, scale_log2, m, l, o, lane);

@@ -36,11 +36,18 @@ def timeit(fn, iters=20, warmup=3):
 
 
 def main():
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="qwen3-14b")
     ap.add_argument("--ms", default="16,40,80,128,160,192")
     ap.add_argument("--ctx", type=int, default=1700)
+    ap.add_argument("--tunable", action="store_true", help="PyTorch TunableOp for the hipBLASLt GEMMs")
+    ap.add_argument("--skip-gemm", action="store_true")
     args = ap.parse_args()
+    if args.tunable:
+        torch.cuda.tunable.enable(True)
+        torch.cuda.tunable.tuning_enable(True)
+        torch.cuda.tunable.set_filename(os.path.join(ROOT, "gpurun_out", "tunableop_results.csv"))
     hip = get_ops("hip")
     cfg = get_model_config(args.model)
     H, I, hd = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim
@@ -48,14 +55,14 @@ def main():
               "gate_up": (2 * I, H), "down": (H, I), "lm_head": (cfg.vocab_size, H)}
     weights = {k: torch.randn(n, kk, device="cuda", dtype=torch.bfloat16) * 0.02 for k, (n, kk) in shapes.items()}
     out = {"model": cfg.name, "gemm": [], "attention": [], "sample": []}
-    for M in [int(m) for m in args.ms.split(",")]:
+    for M in ([] if args.skip_gemm else [int(m) for m in args.ms.split(",")]):
         x = {k: torch.randn(M, kk, device="cuda", dtype=torch.bfloat16) for k, (n, kk) in shapes.items()}
         for name, w in weights.items():
-            t_sk = timeit(lambda: hip.linear(x[name], w))
+            t_sk = timeit(lambda: hip.linear(x[name], w)) if os.environ.get("BCG_SKINNY_GEMM") == "1" else 0.0
             t_bl = timeit(lambda: torch.nn.functional.linear(x[name], w))
             gb = w.numel() * 2 / 1e9
             rec = {"M": M, "op": name, "skinny_us": round(t_sk, 1), "hipblaslt_us": round(t_bl, 1),
-                   "skinny_TBps": round(gb / t_sk * 1e3, 2), "hipblaslt_TBps": round(gb / t_bl * 1e3, 2)}
+                   "skinny_TBps": round(gb / t_sk * 1e3, 2) if t_sk else None, "hipblaslt_TBps": round(gb / t_bl * 1e3, 2)}
             out["gemm"].append(rec)
             print(json.dumps(rec), flush=True)
     # decode attention at the bench geometry
@@ -94,6 +101,8 @@ def main():
         rec = {"B": B, "V": V, "us": round(t, 1)}
         out["sample"].append(rec)
         print(json.dumps(rec), flush=True)
+    if args.tunable:
+        torch.cuda.tunable.write_file()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "bench_ops.json"), "w") as fh:
         json.dump(out, fh, indent=1)
