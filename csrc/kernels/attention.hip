@@ -19,11 +19,11 @@
 //   are 16 contiguous bytes of one V^T row (block h>>1, offset 8(h&1)).
 //   K tiles load row r from token 8(r>>2) + 4u + (r&3) (a row gather: free).
 //
-// Decode: one workgroup per (sequence, kv head, 512-token split); the G = n_q/n_kv
-// query heads of the kv head share every K/V byte (GQA packing: 5 for Qwen3-14B).
-// 4 waves x 128 tokens with the next chunk's K/V loads in flight while the
-// current chunk computes; waves combined through LDS, splits merged by a second
-// kernel (flash-decoding).  Prefill: one workgroup per (64-query tile, query
+// Decode: one workgroup per (sequence, kv head, split of 4 waves x CPW chunks);
+// the G = n_q/n_kv query heads of the kv head share every K/V byte (GQA
+// packing: 5 for Qwen3-14B).  The next chunk's K/V loads are in flight while
+// the current chunk computes; waves are combined through LDS and splits merged
+// by a second kernel (flash-decoding).  Prefill: one workgroup per (64-query tile, query
 // head), causal over cached prefix + new tokens, varlen via a tile table.
 
 #include "common.h"
@@ -31,8 +31,7 @@
 namespace {
 
 constexpr int BS = 16;            // KV block size (tokens)
-constexpr int SPLIT = 512;        // decode tokens per workgroup
-constexpr int DEC_WAVES = 4;
+constexpr int DEC_WAVES = 4;      // decode split = DEC_WAVES * CPW * CHUNK tokens
 constexpr int CHUNK = 32;
 constexpr float LOG2E = 1.4426950408889634f;
 
@@ -149,11 +148,17 @@ struct Causal {
 };
 
 // ------------------------------------------------------------------ decode
-template <int HD>
+// CPW = 32-token chunks per wave; the workgroup's split is 4 * CPW * 32 tokens.
+// The next chunk's loads are issued UNCONDITIONALLY before the current chunk is
+// computed (clamped to the last chunk, a cache hit): a conditional load block
+// makes hipcc merge two vmcnt histories and wait for the prefetch too.
+template <int HD, int CPW>
 __global__ __launch_bounds__(256) void decode_attn_kernel(
     const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
     const int* __restrict__ seq_lens, int n_q, float scale_log2, float* __restrict__ part_o,
     float* __restrict__ part_ml, int max_splits) {
+  constexpr int PER_WAVE = CPW * CHUNK;
+  constexpr int SPLIT = DEC_WAVES * PER_WAVE;
   const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int ctx = seq_lens[b];
   const int start = split * SPLIT;
@@ -171,33 +176,27 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
 #pragma unroll
   for (int dt = 0; dt < HD / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  constexpr int PER_WAVE = SPLIT / DEC_WAVES;  // 128 tokens = 4 chunks = 8 blocks
   const int wbeg = start + w * PER_WAVE;
   const int wend = min(ctx, wbeg + PER_WAVE);
   if (wbeg < wend) {
-    // Block ids of this wave's 8 blocks: one load per lane up front, then broadcast
-    // with readlane -- a table load inside the chunk loop would sit behind the
-    // previous chunk's K/V loads on the in-order vmcnt counter and serialise it.
+    // Block ids of this wave's blocks: one load per lane up front, broadcast with
+    // readlane -- a table load inside the chunk loop would sit behind the previous
+    // chunk's K/V loads on the in-order vmcnt counter and serialise the loop.
     const int nblk = (wend - wbeg + BS - 1) / BS;
+    const int nchunk = (wend - wbeg + CHUNK - 1) / CHUNK;
     const int my_blk = lane < nblk ? table[wbeg / BS + lane] : 0;
+    auto blk = [&](int i) { return __builtin_amdgcn_readlane(my_blk, min(i, nblk - 1)); };
     Chunk<HD> cur, nxt;
-    {
-      const int b0 = __builtin_amdgcn_readlane(my_blk, 0);
-      const int b1 = nblk > 1 ? __builtin_amdgcn_readlane(my_blk, 1) : b0;
-      load_chunk<HD>(cur, g, b0, b1, kvh, lane);
-    }
+    load_chunk<HD>(cur, g, blk(0), blk(1), kvh, lane);
 #pragma unroll
-    for (int c = 0; c < PER_WAVE / CHUNK; ++c) {
-      const int t0 = wbeg + c * CHUNK;
-      if (t0 >= wend) break;
-      const bool more = t0 + CHUNK < wend;
-      if (more) {
-        const int b0 = __builtin_amdgcn_readlane(my_blk, 2 * c + 2);
-        const int b1 = 2 * c + 3 < nblk ? __builtin_amdgcn_readlane(my_blk, 2 * c + 3) : b0;
-        load_chunk<HD>(nxt, g, b0, b1, kvh, lane);
+    for (int c = 0; c < CPW; ++c) {
+      if (c >= nchunk) break;
+      if constexpr (CPW > 1) {
+        const int cn = min(c + 1, nchunk - 1);
+        load_chunk<HD>(nxt, g, blk(2 * cn), blk(2 * cn + 1), kvh, lane);
       }
-      compute_chunk<HD>(cur, bq, t0, ctx, AllVisible{}, scale_log2, m, l, o, lane);
-      if (more) cur = nxt;
+      compute_chunk<HD>(cur, bq, wbeg + c * CHUNK, ctx, AllVisible{}, scale_log2, m, l, o, lane);
+      if constexpr (CPW > 1) cur = nxt;
     }
   }
 
@@ -239,11 +238,12 @@ template <int HD>
 __global__ __launch_bounds__(HD) void decode_combine_kernel(const float* __restrict__ part_o,
                                                             const float* __restrict__ part_ml,
                                                             const int* __restrict__ seq_lens, int n_q,
-                                                            int max_splits, bf16_t* __restrict__ out) {
+                                                            int max_splits, int split_tokens,
+                                                            bf16_t* __restrict__ out) {
   const int bq = blockIdx.x;  // b * n_q + qh
   const int b = bq / n_q;
   const int d = threadIdx.x;
-  const int ns = (seq_lens[b] + SPLIT - 1) / SPLIT;
+  const int ns = (seq_lens[b] + split_tokens - 1) / split_tokens;
   const float* ml = part_ml + static_cast<size_t>(bq) * max_splits * 2;
   float mm = -INFINITY;
   for (int s = 0; s < ns; ++s) mm = fmaxf(mm, ml[2 * s]);
@@ -254,6 +254,20 @@ __global__ __launch_bounds__(HD) void decode_combine_kernel(const float* __restr
     oo += part_o[(static_cast<size_t>(bq) * max_splits + s) * HD + d] * f;
   }
   out[static_cast<size_t>(bq) * HD + d] = f2bf(ll > 0.f ? oo / ll : 0.f);
+}
+
+template <int HD, int CPW>
+int launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks, const int* seq_lens, int B,
+                  int n_q, float sl, float* ws, int max_splits, bf16_t* out, hipStream_t stream) {
+  constexpr int SPLIT = DEC_WAVES * CPW * CHUNK;
+  if (max_splits * SPLIT < max_blocks * BS) return -3;
+  float* part_o = ws;
+  float* part_ml = ws + static_cast<size_t>(B) * n_q * max_splits * HD;
+  hipLaunchKernelGGL((decode_attn_kernel<HD, CPW>), dim3(max_splits, g.n_kv, B), dim3(256), 0, stream, q, g,
+                     tables, max_blocks, seq_lens, n_q, sl, part_o, part_ml, max_splits);
+  hipLaunchKernelGGL(decode_combine_kernel<HD>, dim3(B * n_q), dim3(HD), 0, stream, part_o, part_ml, seq_lens,
+                     n_q, max_splits, SPLIT, out);
+  return 0;
 }
 
 // ----------------------------------------------------------------- prefill
@@ -300,22 +314,15 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
     }
     return __builtin_amdgcn_readlane(my_blk, bi - win_base);
   };
+  // next-chunk loads issued unconditionally (clamped to the last chunk) -- see decode
+  const int nchunk = (kv_end + CHUNK - 1) / CHUNK;
   Chunk<HD> cur, nxt;
-  {
-    const int b0 = block_at(0);
-    const int b1 = nblk > 1 ? block_at(1) : b0;
-    load_chunk<HD>(cur, g, b0, b1, kvh, lane);
-  }
-  for (int t0 = 0; t0 < kv_end; t0 += CHUNK) {
-    const bool more = t0 + CHUNK < kv_end;
-    if (more) {
-      const int bi = (t0 + CHUNK) / BS;
-      const int b0 = block_at(bi);
-      const int b1 = bi + 1 < nblk ? block_at(bi + 1) : b0;
-      load_chunk<HD>(nxt, g, b0, b1, kvh, lane);
-    }
-    compute_chunk<HD>(cur, bq, t0, kv_end, Causal{my_pos}, scale_log2, m, l, o, lane);
-    if (more) cur = nxt;
+  load_chunk<HD>(cur, g, block_at(0), block_at(min(1, nblk - 1)), kvh, lane);
+  for (int c = 0; c < nchunk; ++c) {
+    const int cn = min(c + 1, nchunk - 1);
+    load_chunk<HD>(nxt, g, block_at(2 * cn), block_at(min(2 * cn + 1, nblk - 1)), kvh, lane);
+    compute_chunk<HD>(cur, bq, c * CHUNK, kv_end, Causal{my_pos}, scale_log2, m, l, o, lane);
+    cur = nxt;
   }
   if (!row_ok) return;
   const float inv = l > 0.f ? 1.f / l : 0.f;
@@ -332,7 +339,15 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
 
 }  // namespace
 
-BCG_API int bcg_decode_split_tokens() { return SPLIT; }
+static int g_decode_cpw = 2;  // chunks per wave (1, 2 or 4); split = 128 * cpw tokens
+
+BCG_API int bcg_set_decode_variant(int cpw) {
+  if (cpw != 1 && cpw != 2 && cpw != 4) return -2;
+  g_decode_cpw = cpw;
+  return 0;
+}
+
+BCG_API int bcg_decode_split_tokens() { return DEC_WAVES * CHUNK * g_decode_cpw; }
 
 BCG_API int bcg_paged_attention_decode(const void* q, const void* k_cache, const void* v_cache, int layer,
                                        int num_blocks, int n_kv, const int* block_tables, int max_blocks,
@@ -340,25 +355,18 @@ BCG_API int bcg_paged_attention_decode(const void* q, const void* k_cache, const
                                        float scale, float* workspace, int max_splits, void* out,
                                        hipStream_t stream) {
   if (block_size != BS || n_q % n_kv || n_q / n_kv > 16 || B <= 0) return -2;
-  if (max_splits * SPLIT < max_blocks * BS) return -3;
   KVGeom g{static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), layer, num_blocks, n_kv};
-  float* part_o = workspace;
-  float* part_ml = workspace + static_cast<size_t>(B) * n_q * max_splits * hd;
+  const bf16_t* qb = static_cast<const bf16_t*>(q);
+  bf16_t* ob = static_cast<bf16_t*>(out);
   const float sl = scale * LOG2E;
-  dim3 grid(max_splits, n_kv, B);
-  if (hd == 128) {
-    hipLaunchKernelGGL(decode_attn_kernel<128>, grid, dim3(256), 0, stream, static_cast<const bf16_t*>(q), g,
-                       block_tables, max_blocks, seq_lens, n_q, sl, part_o, part_ml, max_splits);
-    hipLaunchKernelGGL(decode_combine_kernel<128>, dim3(B * n_q), dim3(128), 0, stream, part_o, part_ml,
-                       seq_lens, n_q, max_splits, static_cast<bf16_t*>(out));
-  } else if (hd == 64) {
-    hipLaunchKernelGGL(decode_attn_kernel<64>, grid, dim3(256), 0, stream, static_cast<const bf16_t*>(q), g,
-                       block_tables, max_blocks, seq_lens, n_q, sl, part_o, part_ml, max_splits);
-    hipLaunchKernelGGL(decode_combine_kernel<64>, dim3(B * n_q), dim3(64), 0, stream, part_o, part_ml,
-                       seq_lens, n_q, max_splits, static_cast<bf16_t*>(out));
-  } else {
-    return -2;
-  }
+  int rc = -2;
+#define BCG_DEC(HD_, CPW_)                                                                                  \
+  if (hd == HD_ && g_decode_cpw == CPW_)                                                                    \
+    rc = launch_decode<HD_, CPW_>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace, max_splits, \
+                                  ob, stream);
+  BCG_DEC(128, 1) BCG_DEC(128, 2) BCG_DEC(128, 4) BCG_DEC(64, 1) BCG_DEC(64, 2) BCG_DEC(64, 4)
+#undef BCG_DEC
+  if (rc != 0) return rc;
   return BCG_CHECK_LAUNCH();
 }
 

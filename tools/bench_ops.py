@@ -69,7 +69,8 @@ def main():
     NB = 1 + (args.ctx // 16 + 1) * 192
     k = torch.randn(1, NB, cfg.num_kv_heads, 16, hd, device="cuda", dtype=torch.bfloat16)
     v = torch.randn(1, NB, cfg.num_kv_heads, hd, 16, device="cuda", dtype=torch.bfloat16)
-    for B in (40, 160, 192):
+    for B, cpw in [(b, c) for b in (40, 160, 192) for c in (1, 2, 4)]:
+        hip.set_decode_variant(cpw)
         nb = (args.ctx + 15) // 16
         tables = (torch.arange(B * nb, dtype=torch.int32, device="cuda").view(B, nb) + 1)
         tables = torch.cat([tables, torch.zeros(B, 512 - nb, dtype=torch.int32, device="cuda")], 1).contiguous()
@@ -77,7 +78,7 @@ def main():
         q = torch.randn(B, cfg.num_heads, hd, device="cuda", dtype=torch.bfloat16)
         t = timeit(lambda: hip.paged_attention_decode(q, k, v, 0, tables, seq, hd ** -0.5))
         gb = B * args.ctx * cfg.num_kv_heads * hd * 2 * 2 / 1e9
-        rec = {"B": B, "ctx": args.ctx, "us": round(t, 1), "TBps": round(gb / t * 1e3, 2)}
+        rec = {"B": B, "ctx": args.ctx, "cpw": cpw, "us": round(t, 1), "TBps": round(gb / t * 1e3, 2)}
         out["attention"].append(rec)
         print(json.dumps(rec), flush=True)
     # sampler
@@ -102,7 +103,7 @@ def main():
         out["sample"].append(rec)
         print(json.dumps(rec), flush=True)
     if args.tunable:
-        torch.cuda.tunable.write_file()
+        torch.cuda.tunable.write_file() if hasattr(torch.cuda.tunable, "write_file") else None
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "bench_ops.json"), "w") as fh:
         json.dump(out, fh, indent=1)
