@@ -37,12 +37,11 @@ def load_library(path: str = None) -> ctypes.CDLL:
                                       c_float, c_void_p],
         "bcg_paged_attention_decode": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                        c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int,
-                                       c_void_p, c_void_p],
+                                       c_int, c_void_p, c_void_p],
         "bcg_paged_attention_prefill": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                                         c_void_p, c_void_p],
-        "bcg_decode_split_tokens": [],
-        "bcg_set_decode_variant": [c_int],
+        "bcg_decode_split_tokens": [c_int, c_int, c_int],
         "bcg_gemm_skinny": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                             c_void_p],
         "bcg_guided_sample": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -77,7 +76,6 @@ def _req(cond: bool, msg: str):
 
 def hip_ops() -> SimpleNamespace:
     lib = load_library()
-    _check(lib.bcg_set_decode_variant(int(os.environ.get("BCG_DECODE_CPW", "2"))), "set_decode_variant")
 
     def add_rmsnorm(x, residual, w, eps):
         _req(x.dtype == torch.bfloat16 and x.is_contiguous() and x.dim() == 2, "add_rmsnorm: x bf16 [T,H]")
@@ -126,13 +124,13 @@ def hip_ops() -> SimpleNamespace:
         _req(q.is_contiguous() and block_tables.dtype == torch.int32 and block_tables.is_contiguous()
              and block_tables.shape[0] == B and seq_lens.numel() == B, "decode attention inputs")
         max_blocks = block_tables.shape[1]
-        split = lib.bcg_decode_split_tokens()
+        split = lib.bcg_decode_split_tokens(B, n_kv, max_blocks * BS)
         max_splits = (max_blocks * BS + split - 1) // split
         ws = torch.empty(B * n_q * max_splits * (hd + 2), dtype=torch.float32, device=q.device)
         out = torch.empty(B, n_q * hd, dtype=q.dtype, device=q.device)
         _check(lib.bcg_paged_attention_decode(
             _p(q), _p(k_cache), _p(v_cache), layer, NB, n_kv, _p(block_tables), max_blocks, _p(seq_lens),
-            B, n_q, hd, BS, scale, _p(ws), max_splits, _p(out), _stream()), "paged_attention_decode")
+            B, n_q, hd, BS, scale, _p(ws), max_splits, split, _p(out), _stream()), "paged_attention_decode")
         return out
 
     def paged_attention_prefill(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale,
@@ -191,10 +189,7 @@ def hip_ops() -> SimpleNamespace:
             out_tokens.shape[1], _p(next_tokens), seed & 0xFFFFFFFF, int(bool(budget_aware)), n_text_tokens,
             eos_id, eos_id2, _stream()), "guided_sample")
 
-    def set_decode_variant(cpw: int):
-        _check(lib.bcg_set_decode_variant(cpw), "set_decode_variant")
-
-    return SimpleNamespace(name="hip", linear=linear, set_decode_variant=set_decode_variant, rmsnorm=rmsnorm, add_rmsnorm=add_rmsnorm, silu_mul=silu_mul,
+    return SimpleNamespace(name="hip", linear=linear, rmsnorm=rmsnorm, add_rmsnorm=add_rmsnorm, silu_mul=silu_mul,
                            qk_norm_rope_kv_write=qk_norm_rope_kv_write,
                            paged_attention_decode=paged_attention_decode,
                            paged_attention_prefill=paged_attention_prefill, sample_step=sample_step,

@@ -19,11 +19,10 @@
 //   are 16 contiguous bytes of one V^T row (block h>>1, offset 8(h&1)).
 //   K tiles load row r from token 8(r>>2) + 4u + (r&3) (a row gather: free).
 //
-// Decode: one workgroup per (sequence, kv head, split of 4 waves x CPW chunks);
-// the G = n_q/n_kv query heads of the kv head share every K/V byte (GQA
-// packing: 5 for Qwen3-14B).  The next chunk's K/V loads are in flight while
-// the current chunk computes; waves are combined through LDS and splits merged
-// by a second kernel (flash-decoding).  Prefill: one workgroup per (64-query tile, query
+// Decode: one workgroup per (sequence, kv head, split); the G = n_q/n_kv query
+// heads of the kv head share every K/V byte (GQA packing: 5 for Qwen3-14B);
+// waves are combined through LDS and splits merged by a second kernel
+// (flash-decoding).  Prefill: one workgroup per (64-query tile, query
 // head), causal over cached prefix + new tokens, varlen via a tile table.
 
 #include "common.h"
@@ -31,7 +30,7 @@
 namespace {
 
 constexpr int BS = 16;            // KV block size (tokens)
-constexpr int DEC_WAVES = 4;      // decode split = DEC_WAVES * CPW * CHUNK tokens
+constexpr int DEC_WAVES = 4;
 constexpr int CHUNK = 32;
 constexpr float LOG2E = 1.4426950408889634f;
 
@@ -148,20 +147,22 @@ struct Causal {
 };
 
 // ------------------------------------------------------------------ decode
-// CPW = 32-token chunks per wave; the workgroup's split is 4 * CPW * 32 tokens.
-// The next chunk's loads are issued UNCONDITIONALLY before the current chunk is
-// computed (clamped to the last chunk, a cache hit): a conditional load block
-// makes hipcc merge two vmcnt histories and wait for the prefetch too.
-template <int HD, int CPW>
+// One workgroup per (sequence, kv head, split); a split is `split_tokens`
+// (multiple of 128) tokens, chosen per launch so that B * n_kv * splits keeps
+// every CU busy (large B => 1-2 splits => little partial-sum traffic).  The 4
+// waves take the split's 32-token chunks round-robin; each wave keeps ONE chunk
+// in registers (~64 VGPRs) so 3-4 waves per SIMD stay resident and hide the HBM
+// latency.  Block ids of a wave's chunks are fetched once (lane i holds chunk
+// i's two block ids) and broadcast with readlane, so no table load sits between
+// K/V loads on the in-order vmcnt counter.
+template <int HD>
 __global__ __launch_bounds__(256) void decode_attn_kernel(
     const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
     const int* __restrict__ seq_lens, int n_q, float scale_log2, float* __restrict__ part_o,
-    float* __restrict__ part_ml, int max_splits) {
-  constexpr int PER_WAVE = CPW * CHUNK;
-  constexpr int SPLIT = DEC_WAVES * PER_WAVE;
+    float* __restrict__ part_ml, int max_splits, int split_tokens) {
   const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int ctx = seq_lens[b];
-  const int start = split * SPLIT;
+  const int start = split * split_tokens;
   if (start >= ctx) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, h = lane >> 4;
@@ -176,28 +177,21 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
 #pragma unroll
   for (int dt = 0; dt < HD / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int wbeg = start + w * PER_WAVE;
-  const int wend = min(ctx, wbeg + PER_WAVE);
-  if (wbeg < wend) {
-    // Block ids of this wave's blocks: one load per lane up front, broadcast with
-    // readlane -- a table load inside the chunk loop would sit behind the previous
-    // chunk's K/V loads on the in-order vmcnt counter and serialise the loop.
-    const int nblk = (wend - wbeg + BS - 1) / BS;
-    const int nchunk = (wend - wbeg + CHUNK - 1) / CHUNK;
-    const int my_blk = lane < nblk ? table[wbeg / BS + lane] : 0;
-    auto blk = [&](int i) { return __builtin_amdgcn_readlane(my_blk, min(i, nblk - 1)); };
-    Chunk<HD> cur, nxt;
-    load_chunk<HD>(cur, g, blk(0), blk(1), kvh, lane);
-#pragma unroll
-    for (int c = 0; c < CPW; ++c) {
-      if (c >= nchunk) break;
-      if constexpr (CPW > 1) {
-        const int cn = min(c + 1, nchunk - 1);
-        load_chunk<HD>(nxt, g, blk(2 * cn), blk(2 * cn + 1), kvh, lane);
-      }
-      compute_chunk<HD>(cur, bq, wbeg + c * CHUNK, ctx, AllVisible{}, scale_log2, m, l, o, lane);
-      if constexpr (CPW > 1) cur = nxt;
-    }
+  const int end = min(ctx, start + split_tokens);
+  const int nchunk = (end - start + CHUNK - 1) / CHUNK;     // chunks of this split
+  const int mine = (nchunk - w + DEC_WAVES - 1) / DEC_WAVES;  // chunks of this wave (<= 64)
+  const int last_blk = (ctx - 1) / BS;
+  int e0 = 0, e1 = 0;
+  if (lane < mine) {
+    const int t0 = start + (w + lane * DEC_WAVES) * CHUNK;
+    e0 = table[t0 / BS];
+    e1 = table[min(t0 / BS + 1, last_blk)];
+  }
+  for (int i = 0; i < mine; ++i) {
+    const int t0 = start + (w + i * DEC_WAVES) * CHUNK;
+    Chunk<HD> c;
+    load_chunk<HD>(c, g, __builtin_amdgcn_readlane(e0, i), __builtin_amdgcn_readlane(e1, i), kvh, lane);
+    compute_chunk<HD>(c, bq, t0, end, AllVisible{}, scale_log2, m, l, o, lane);
   }
 
   // combine the 4 waves through LDS
@@ -256,18 +250,15 @@ __global__ __launch_bounds__(HD) void decode_combine_kernel(const float* __restr
   out[static_cast<size_t>(bq) * HD + d] = f2bf(ll > 0.f ? oo / ll : 0.f);
 }
 
-template <int HD, int CPW>
-int launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks, const int* seq_lens, int B,
-                  int n_q, float sl, float* ws, int max_splits, bf16_t* out, hipStream_t stream) {
-  constexpr int SPLIT = DEC_WAVES * CPW * CHUNK;
-  if (max_splits * SPLIT < max_blocks * BS) return -3;
+template <int HD>
+void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks, const int* seq_lens, int B,
+                   int n_q, float sl, float* ws, int max_splits, int split_tokens, bf16_t* out, hipStream_t stream) {
   float* part_o = ws;
   float* part_ml = ws + static_cast<size_t>(B) * n_q * max_splits * HD;
-  hipLaunchKernelGGL((decode_attn_kernel<HD, CPW>), dim3(max_splits, g.n_kv, B), dim3(256), 0, stream, q, g,
-                     tables, max_blocks, seq_lens, n_q, sl, part_o, part_ml, max_splits);
+  hipLaunchKernelGGL(decode_attn_kernel<HD>, dim3(max_splits, g.n_kv, B), dim3(256), 0, stream, q, g, tables,
+                     max_blocks, seq_lens, n_q, sl, part_o, part_ml, max_splits, split_tokens);
   hipLaunchKernelGGL(decode_combine_kernel<HD>, dim3(B * n_q), dim3(HD), 0, stream, part_o, part_ml, seq_lens,
-                     n_q, max_splits, SPLIT, out);
-  return 0;
+                     n_q, max_splits, split_tokens, out);
 }
 
 // ----------------------------------------------------------------- prefill
@@ -339,34 +330,37 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
 
 }  // namespace
 
-static int g_decode_cpw = 2;  // chunks per wave (1, 2 or 4); split = 128 * cpw tokens
-
-BCG_API int bcg_set_decode_variant(int cpw) {
-  if (cpw != 1 && cpw != 2 && cpw != 4) return -2;
-  g_decode_cpw = cpw;
-  return 0;
+// Split size (tokens, power of two in [128, 4096]) for a decode batch.  BCG
+// contexts are ~1-3k tokens, so split ~= B * n_kv keeps B * n_kv * ctx/split
+// around 2k workgroups (8 per CU) at ctx ~2k; independent of the actual
+// lengths, so a captured HIP graph stays valid as the sequences grow.
+BCG_API int bcg_decode_split_tokens(int B, int n_kv, int max_tokens) {
+  int split = 128;
+  while (split < 4096 && split * 2 <= B * n_kv && split < max_tokens) split *= 2;
+  return split;
 }
-
-BCG_API int bcg_decode_split_tokens() { return DEC_WAVES * CHUNK * g_decode_cpw; }
 
 BCG_API int bcg_paged_attention_decode(const void* q, const void* k_cache, const void* v_cache, int layer,
                                        int num_blocks, int n_kv, const int* block_tables, int max_blocks,
                                        const int* seq_lens, int B, int n_q, int hd, int block_size,
-                                       float scale, float* workspace, int max_splits, void* out,
-                                       hipStream_t stream) {
+                                       float scale, float* workspace, int max_splits, int split_tokens,
+                                       void* out, hipStream_t stream) {
   if (block_size != BS || n_q % n_kv || n_q / n_kv > 16 || B <= 0) return -2;
+  if (split_tokens % 128 || split_tokens > DEC_WAVES * 64 * CHUNK || max_splits * split_tokens < max_blocks * BS)
+    return -3;
   KVGeom g{static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), layer, num_blocks, n_kv};
   const bf16_t* qb = static_cast<const bf16_t*>(q);
   bf16_t* ob = static_cast<bf16_t*>(out);
   const float sl = scale * LOG2E;
-  int rc = -2;
-#define BCG_DEC(HD_, CPW_)                                                                                  \
-  if (hd == HD_ && g_decode_cpw == CPW_)                                                                    \
-    rc = launch_decode<HD_, CPW_>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace, max_splits, \
-                                  ob, stream);
-  BCG_DEC(128, 1) BCG_DEC(128, 2) BCG_DEC(128, 4) BCG_DEC(64, 1) BCG_DEC(64, 2) BCG_DEC(64, 4)
-#undef BCG_DEC
-  if (rc != 0) return rc;
+  if (hd == 128) {
+    launch_decode<128>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace, max_splits, split_tokens,
+                       ob, stream);
+  } else if (hd == 64) {
+    launch_decode<64>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace, max_splits, split_tokens,
+                      ob, stream);
+  } else {
+    return -2;
+  }
   return BCG_CHECK_LAUNCH();
 }
 

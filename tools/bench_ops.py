@@ -69,8 +69,7 @@ def main():
     NB = 1 + (args.ctx // 16 + 1) * 192
     k = torch.randn(1, NB, cfg.num_kv_heads, 16, hd, device="cuda", dtype=torch.bfloat16)
     v = torch.randn(1, NB, cfg.num_kv_heads, hd, 16, device="cuda", dtype=torch.bfloat16)
-    for B, cpw in [(b, c) for b in (40, 160, 192) for c in (1, 2, 4)]:
-        hip.set_decode_variant(cpw)
+    for B in (8, 40, 160, 192):
         nb = (args.ctx + 15) // 16
         tables = (torch.arange(B * nb, dtype=torch.int32, device="cuda").view(B, nb) + 1)
         tables = torch.cat([tables, torch.zeros(B, 512 - nb, dtype=torch.int32, device="cuda")], 1).contiguous()
@@ -78,7 +77,7 @@ def main():
         q = torch.randn(B, cfg.num_heads, hd, device="cuda", dtype=torch.bfloat16)
         t = timeit(lambda: hip.paged_attention_decode(q, k, v, 0, tables, seq, hd ** -0.5))
         gb = B * args.ctx * cfg.num_kv_heads * hd * 2 * 2 / 1e9
-        rec = {"B": B, "ctx": args.ctx, "cpw": cpw, "us": round(t, 1), "TBps": round(gb / t * 1e3, 2)}
+        rec = {"B": B, "ctx": args.ctx, "us": round(t, 1), "TBps": round(gb / t * 1e3, 2)}
         out["attention"].append(rec)
         print(json.dumps(rec), flush=True)
     # sampler
