@@ -66,6 +66,9 @@ __device__ __forceinline__ void load_chunk(Chunk<HD>& c, const KVGeom& g, int bl
   const bf16_t* vb = g.v + (h < 2 ? b0 : b1) + 8 * (h & 1);
 #pragma unroll
   for (int dt = 0; dt < HD / 16; ++dt) c.v[dt] = *reinterpret_cast<const bf16x8*>(vb + (dt * 16 + r) * BS);
+  // Keep all 16 loads of the chunk together: without this fence hipcc sinks the
+  // V loads below the S^T MFMAs that wait for K, i.e. two serial HBM round trips.
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // Online-softmax update + O^T accumulation for one chunk starting at token t0.
@@ -112,17 +115,21 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD>& c, const bf16x8 (
 #pragma unroll
   for (int j = 0; j < 8; ++j) bp[j] = static_cast<__bf16>(p[j]);
   // tokens past kv_end may hold stale (even non-finite) bytes: zero their V
-  const bool v_ok = t0 + 8 * h + 7 < kv_end;
+  // with branch-free 32-bit masks (a divergent branch here splits the vmcnt waits)
+  uint32_t keep[4];
+#pragma unroll
+  for (int j2 = 0; j2 < 4; ++j2) {
+    const int t = t0 + 8 * h + 2 * j2;
+    keep[j2] = (t < kv_end ? 0x0000ffffu : 0u) | (t + 1 < kv_end ? 0xffff0000u : 0u);
+  }
 #pragma unroll
   for (int dt = 0; dt < HD / 16; ++dt) {
     o[dt] *= alpha;
-    bf16x8 va = c.v[dt];
-    if (!v_ok) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 va = __builtin_bit_cast(u32x4, c.v[dt]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (t0 + 8 * h + j >= kv_end) va[j] = static_cast<__bf16>(0.f);
-    }
-    o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, bp, o[dt], 0, 0, 0);
+    for (int j2 = 0; j2 < 4; ++j2) va[j2] &= keep[j2];
+    o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, va), bp, o[dt], 0, 0, 0);
   }
 }
 
