@@ -138,6 +138,8 @@ class InferenceEngine:
         self.eos_ids = (self.tokenizer.eos_token_ids + [self.tokenizer.eos_token_ids[0]])[:2]
         self.n_text_tokens = min(self.tokenizer.vocab_size, cfg.vocab_size)
         self._alloc_kv_cache()
+        if self.backend == "hip":
+            self._load_tuned_gemms()
         self.graphs = None
         if self.backend == "hip" and args.use_hip_graphs:
             from .graphs import DecodeGraphs
@@ -175,6 +177,28 @@ class InferenceEngine:
         self.num_blocks = num_blocks
         self.max_blocks_per_seq = (a.max_model_len + bs - 1) // bs
         self.kv_bytes = 2 * self.k_cache.numel() * self.k_cache.element_size()
+
+    def _load_tuned_gemms(self):
+        """Load PyTorch TunableOp results for this model's decode GEMM shapes (lookups only).
+
+        ``tools/tune_gemms.py`` times every hipBLASLt/rocBLAS solution per decode
+        bucket; e.g. Qwen3-14B down_proj at M=160 goes 126 -> 54 us.  Unknown
+        shapes (prefill) fall back to the library default, no tuning at run time.
+        """
+        if os.environ.get("BCG_TUNABLEOP", "1") == "0":
+            return
+        name = self.args.model.split("/")[-1].lower()
+        path = os.path.join(os.path.dirname(__file__), "tuned",
+                            f"tunableop_{name}_tp{self.args.tensor_parallel_size}.csv")
+        if not os.path.exists(path):
+            return
+        import tempfile
+        t = torch.cuda.tunable
+        t.enable(True)
+        t.tuning_enable(False)
+        t.set_filename(os.path.join(tempfile.gettempdir(), f"bcg_tunableop_{os.getpid()}.csv"))
+        t.read_file(path)
+        self.tuned_gemm_file = path
 
     def _phys(self, blocks: List[int]) -> List[int]:
         return [b + 1 for b in blocks]  # manager ids are shifted past scratch block 0

@@ -118,13 +118,15 @@ def hip_ops() -> SimpleNamespace:
             n_q, n_kv, head_dim, NB, BS, eps, _stream()), "qk_norm_rope_kv_write")
         return q
 
+    _split_override = int(os.environ.get("BCG_DECODE_SPLIT", "0"))
+
     def paged_attention_decode(q, k_cache, v_cache, layer, block_tables, seq_lens, scale):
         B, n_q, hd = q.shape
         L, NB, n_kv, BS, _ = k_cache.shape
         _req(q.is_contiguous() and block_tables.dtype == torch.int32 and block_tables.is_contiguous()
              and block_tables.shape[0] == B and seq_lens.numel() == B, "decode attention inputs")
         max_blocks = block_tables.shape[1]
-        split = lib.bcg_decode_split_tokens(B, n_kv, max_blocks * BS)
+        split = _split_override or lib.bcg_decode_split_tokens(B, n_kv, max_blocks * BS)
         max_splits = (max_blocks * BS + split - 1) // split
         ws = torch.empty(B * n_q * max_splits * (hd + 2), dtype=torch.float32, device=q.device)
         out = torch.empty(B, n_q * hd, dtype=q.dtype, device=q.device)

@@ -337,15 +337,13 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
 
 }  // namespace
 
-// Split size (tokens, power of two in [128, 4096]) for a decode batch.  BCG
-// contexts are ~1-3k tokens, so split ~= B * n_kv keeps B * n_kv * ctx/split
-// around 2k workgroups (8 per CU) at ctx ~2k; independent of the actual
-// lengths, so a captured HIP graph stays valid as the sequences grow.
-BCG_API int bcg_decode_split_tokens(int B, int n_kv, int max_tokens) {
-  int split = 128;
-  while (split < 4096 && split * 2 <= B * n_kv && split < max_tokens) split *= 2;
-  return split;
-}
+// Split size for a decode batch.  Measured on MI355X (tools/bench_ops.py,
+// Qwen3-14B geometry, ctx 1700, B 40-192): one 32-token chunk per wave (128
+// tokens per workgroup) reaches 3.0-3.2 TB/s; looping waves over several
+// chunks (256-2048-token splits) stays at 2.0-2.6 TB/s even with every chunk's
+// 16 loads issued together -- short-lived workgroups keep more loads in
+// flight per CU than long ones at 3 waves/SIMD.
+BCG_API int bcg_decode_split_tokens(int B, int n_kv, int max_tokens) { return 128; }
 
 BCG_API int bcg_paged_attention_decode(const void* q, const void* k_cache, const void* v_cache, int layer,
                                        int num_blocks, int n_kv, const int* block_tables, int max_blocks,

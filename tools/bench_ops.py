@@ -69,7 +69,7 @@ def main():
     NB = 1 + (args.ctx // 16 + 1) * 192
     k = torch.randn(1, NB, cfg.num_kv_heads, 16, hd, device="cuda", dtype=torch.bfloat16)
     v = torch.randn(1, NB, cfg.num_kv_heads, hd, 16, device="cuda", dtype=torch.bfloat16)
-    for B in (8, 40, 160, 192):
+    for B in [int(b) for b in os.environ.get("BCG_BENCH_B", "8,40,160,192").split(",")]:
         nb = (args.ctx + 15) // 16
         tables = (torch.arange(B * nb, dtype=torch.int32, device="cuda").view(B, nb) + 1)
         tables = torch.cat([tables, torch.zeros(B, 512 - nb, dtype=torch.int32, device="cuda")], 1).contiguous()
