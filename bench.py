@@ -2,14 +2,15 @@
 
 Metric (BASELINE.md "Measurement protocol"): accepted decide outputs +
 accepted vote outputs per wall-clock second, summed over every GPU of the
-node.  One "step" = one BCG round of every simulation running on the GPU:
-all agents' decide prompts in ONE engine call, all vote prompts in ONE call,
-plus whatever retries the reference's retry ladder triggers.
+node.  One "step" = one BCG round of every simulation running on the GPU (each
+round: all agents' decide prompts in one engine call, all vote prompts in one
+call, plus whatever retries the reference's retry ladder triggers).
 
 Layout: one process per GPU (torchrun), data-parallel over independent
-simulation seeds (``--sims-per-gpu`` games share each GPU's engine; a game
-that ends is replaced by a fresh seed so the pool stays full).  With
-``--tp > 1`` groups of GPUs form tensor-parallel engines (RCCL all-reduce).
+simulation seeds (``--sims-per-gpu`` games share each GPU's engine, which
+serves them with continuous batching; a game that ends is replaced by a fresh
+seed so the pool stays full).  With ``--tp > 1`` groups of GPUs form
+tensor-parallel engines (RCCL all-reduce) fed by lock-step coalesced rounds.
 
 Data: random-init weights of the real architecture and the synthetic
 byte-level BPE tokenizer (no network for checkpoints); the budget-aware JSON
@@ -58,60 +59,71 @@ def parse():
 
 
 class SimPool:
-    """S simulations advanced in lock-step; each round's engine calls are coalesced."""
+    """S independent simulations, each on its own thread, sharing the engine.
 
-    def __init__(self, llm, n_sims, honest, byzantine, max_rounds, seed, rank):
+    With continuous batching the simulations are NOT in lock-step: one game's
+    retry phase overlaps another game's decide phase, keeping the decode batch
+    full.  A game that ends is replaced by a fresh seed.  ``run(rounds)`` makes
+    every simulation play exactly ``rounds`` rounds.
+    """
+
+    def __init__(self, n_sims, honest, byzantine, max_rounds, seed, rank):
         from byzantine_consensus_llm_agents_amd.bcg.simulation import BCGSimulation
         self.BCGSimulation = BCGSimulation
-        self.llm = llm
         self.honest, self.byzantine, self.max_rounds = honest, byzantine, max_rounds
         self.seed_base = seed * 100003 + rank * 7919
         self.next_seed = 0
+        self.lock = threading.Lock()
         self.sims = [self._new_sim() for _ in range(n_sims)]
         self.games_finished = 0
         self.outcomes = {}
 
     def _new_sim(self):
-        self.next_seed += 1
+        with self.lock:
+            self.next_seed += 1
+            seed = self.seed_base + self.next_seed
         return self.BCGSimulation(self.honest, self.byzantine, config={
             "max_rounds": self.max_rounds, "value_range": (0, 50), "consensus_threshold": 66.0,
-            "verbose": False, "byzantine_awareness": "may_exist", "seed": self.seed_base + self.next_seed})
+            "verbose": False, "byzantine_awareness": "may_exist", "seed": seed})
 
-    def counts(self):
-        return sum(s.counters["decisions_accepted"] + s.counters["votes_accepted"] for s in self.sims)
-
-    def round(self):
-        """One round of every simulation; returns decisions accepted in it."""
-        before = self.counts()
+    def run(self, rounds: int, llm=None, lockstep=False) -> int:
+        """Every simulation plays `rounds` rounds; returns accepted decisions."""
+        made = [0] * len(self.sims)
         errors = []
 
-        def work(sim):
-            threading.current_thread()._bcg_participant = True
+        def work(i):
+            th = threading.current_thread()
+            th._bcg_participant = lockstep
+            th._bcg_order_key = (i,)
             try:
-                sim.run_round()
+                for _ in range(rounds):
+                    sim = self.sims[i]
+                    before = sim.counters["decisions_accepted"] + sim.counters["votes_accepted"]
+                    sim.run_round()
+                    made[i] += sim.counters["decisions_accepted"] + sim.counters["votes_accepted"] - before
+                    if sim.game.game_over:
+                        o = sim.game.get_statistics().get("consensus_outcome")
+                        with self.lock:
+                            self.outcomes[o] = self.outcomes.get(o, 0) + 1
+                            self.games_finished += 1
+                        self.sims[i] = self._new_sim()
             except BaseException as exc:  # surface thread failures
                 errors.append(exc)
             finally:
-                self.llm.unregister_client()
+                if lockstep:
+                    llm.unregister_client()
 
-        for _ in self.sims:
-            self.llm.register_client()
-        threads = [threading.Thread(target=work, args=(s,)) for s in self.sims]
+        if lockstep:
+            for _ in self.sims:
+                llm.register_client()
+        threads = [threading.Thread(target=work, args=(i,)) for i in range(len(self.sims))]
         for t in threads:
             t.start()
         for t in threads:
             t.join()
         if errors:
             raise errors[0]
-        made = self.counts() - before
-        for i, s in enumerate(self.sims):
-            if s.game.game_over:
-                stats = s.game.get_statistics()
-                o = stats.get("consensus_outcome")
-                self.outcomes[o] = self.outcomes.get(o, 0) + 1
-                self.games_finished += 1
-                self.sims[i] = self._new_sim()
-        return made
+        return sum(made)
 
 
 def main():
@@ -148,12 +160,15 @@ def main():
     EngineAgent._shared_model_config = dict(C.VLLM_CONFIG)
     init_s = time.perf_counter() - t0
 
-    pool = SimPool(llm, args.sims_per_gpu, args.honest, args.byzantine, args.max_rounds,
+    lockstep = args.tp > 1  # TP ranks need identical batches: coalesced lock-step rounds
+    if not lockstep:
+        llm.start_continuous_batching()
+    pool = SimPool(args.sims_per_gpu, args.honest, args.byzantine, args.max_rounds,
                    args.seed + rank // args.tp, rank // args.tp)
-    for i in range(args.warmup):
-        n = pool.round()
+    if args.warmup:
+        n = pool.run(args.warmup, llm, lockstep)
         if rank == 0 and args.verbose:
-            print(f"[warmup {i}] decisions={n}", file=sys.stderr, flush=True)
+            print(f"[warmup] {args.warmup} rounds/sim, decisions={n}", file=sys.stderr, flush=True)
 
     eng = getattr(llm.backend, "stats", {})
     stats0 = dict(eng)
@@ -162,13 +177,10 @@ def main():
     if args.backend == "hip":
         torch.cuda.synchronize()
     t_start = time.perf_counter()
-    decisions = 0
-    for i in range(args.steps):
-        n = pool.round()
-        decisions += n
-        if rank == 0:
-            print(f"[round {i}] decisions={n} elapsed={time.perf_counter() - t_start:.2f}s",
-                  file=sys.stderr, flush=True)
+    decisions = pool.run(args.steps, llm, lockstep)
+    if rank == 0:
+        print(f"[timed] {args.steps} rounds/sim decisions={decisions} elapsed={time.perf_counter() - t_start:.2f}s",
+              file=sys.stderr, flush=True)
     if args.backend == "hip":
         torch.cuda.synchronize()
     if world > 1:
@@ -211,6 +223,7 @@ def main():
                        "phases_rank0": llm.backend.timer.summary() if hasattr(llm.backend, "timer") else {}},
         }
         print(json.dumps(line), flush=True)
+    llm.shutdown()
     if world > 1:
         dist.destroy_process_group()
 

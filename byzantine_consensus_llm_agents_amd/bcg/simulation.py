@@ -118,7 +118,10 @@ def run_concurrently(engine_agent, jobs):
     results = [None] * len(jobs)
     errors = []
 
+    parent_key = getattr(threading.current_thread(), "_bcg_order_key", ())
+
     def work(i, job):
+        threading.current_thread()._bcg_order_key = tuple(parent_key) + (i,)
         try:
             results[i] = job()
         except BaseException as exc:

@@ -20,11 +20,12 @@ they are per-row device state (``fsm_base/fsm_state``, ``temperature``,
 ``max_new``).
 """
 
-import math
+import collections
+import contextlib
 import os
-import time
+import threading
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Deque, Dict, List, Optional
 
 import torch
 
@@ -35,6 +36,8 @@ from ..ops import get_ops
 from ..utils.trace import PhaseTimer
 from .guided.compiler import FSMRegistry
 from .tokenizer import load_tokenizer
+
+OUT_WIDTH = 1024  # max generated tokens per sequence (the reference uses <= 300)
 
 
 @dataclass
@@ -61,6 +64,7 @@ class EngineArgs:
     dtype: torch.dtype = torch.bfloat16
     device: Optional[str] = None
     poll_every: int = 8
+    async_mode: bool = False
 
     @classmethod
     def from_configs(cls, model: str, backend: str, weights: Optional[str] = None,
@@ -140,6 +144,10 @@ class InferenceEngine:
         self._alloc_kv_cache()
         if self.backend == "hip":
             self._load_tuned_gemms()
+        self._alloc_state()
+        self._cv = threading.Condition()
+        self._waiting: Deque[_Request] = collections.deque()
+        self.async_mode = False
         self.graphs = None
         if self.backend == "hip" and args.use_hip_graphs:
             from .graphs import DecodeGraphs
@@ -200,123 +208,259 @@ class InferenceEngine:
         t.read_file(path)
         self.tuned_gemm_file = path
 
+    def _alloc_state(self):
+        """Per-row decode state, shared by every graph bucket (bucket b uses rows [0, b))."""
+        from .graphs import MAX_ROWS
+        cap = min(MAX_ROWS, max(self.args.max_batch_seqs, 1))
+        dev = self.device
+        z = lambda: torch.zeros(cap, dtype=torch.int32, device=dev)  # noqa: E731
+        self.state = {
+            "block_tables": torch.zeros(cap, self.max_blocks_per_seq, dtype=torch.int32, device=dev),
+            "seq_lens": torch.ones(cap, dtype=torch.int32, device=dev),
+            "fsm_base": torch.full((cap,), -1, dtype=torch.int32, device=dev),
+            "fsm_state": z(), "gen_count": z(), "max_new": torch.ones(cap, dtype=torch.int32, device=dev),
+            "temperature": torch.zeros(cap, dtype=torch.float32, device=dev), "row_keys": z(),
+            "done": torch.ones(cap, dtype=torch.int32, device=dev), "next_tokens": z(),
+            "out_tokens": torch.zeros(cap, OUT_WIDTH, dtype=torch.int32, device=dev)}
+        self.slots: List[Optional[_Request]] = [None] * cap
+
     def _phys(self, blocks: List[int]) -> List[int]:
         return [b + 1 for b in blocks]  # manager ids are shifted past scratch block 0
 
     # ------------------------------------------------------------ serving
     def generate(self, prompts: List[str], params_list) -> List[str]:
-        # the coalescer may run this on any simulation thread; the current HIP
-        # device (and with it torch.cuda.current_stream used by the ctypes
-        # launches) is thread-local, so pin it for the whole call
-        if self.device.type == "cuda":
-            with torch.cuda.device(self.device):
-                return self._generate(prompts, params_list)
-        return self._generate(prompts, params_list)
+        """Serve one batch of prompts; returns the generated texts in order.
 
-    def _generate(self, prompts: List[str], params_list) -> List[str]:
-        self.stats["calls"] += 1
+        Async mode (continuous batching): the requests join the running batch of
+        the background scheduler thread and this call waits for them.  Sync
+        mode: the calling thread drives the scheduler until they are done.
+        """
+        reqs = self.submit(prompts, params_list)
+        if self.async_mode:
+            for r in reqs:
+                r.event.wait()
+        else:
+            with self._device_ctx():
+                while not all(r.event.is_set() for r in reqs):
+                    self._iterate()
+        for r in reqs:
+            if r.exc is not None:
+                raise r.exc
+        return [r.text for r in reqs]
+
+    def submit(self, prompts: List[str], params_list) -> List["_Request"]:
+        """Tokenise + compile schemas on the caller's thread, enqueue for admission."""
         with self.timer.phase("tokenize"):
             ids = self.tokenizer.encode_batch(prompts)
-        seqs: List[_Seq] = []
-        for i, (p_ids, p) in enumerate(zip(ids, params_list)):
+        reqs = []
+        for p_ids, p in zip(ids, params_list):
             schema = p.guided_decoding.json if p.guided_decoding is not None else None
             with self.timer.phase("fsm_compile"):
                 base = self.fsm.get(schema) if schema is not None else -1
-            s = _Seq(i, p_ids, max(1, int(p.max_tokens)), float(p.temperature), base)
-            if len(p_ids) == 0 or len(p_ids) + s.max_new > self.args.max_model_len:
-                s.error = "prompt too long" if p_ids else "empty prompt"
-            seqs.append(s)
-        texts = [""] * len(seqs)
-        todo = [s for s in seqs if s.error is None]
-        wave_cap = self.args.max_batch_seqs
-        if self.args.honor_max_num_seqs and self.args.max_num_seqs:
-            wave_cap = min(wave_cap, self.args.max_num_seqs)
-        while todo:
-            wave, todo = self._admit(todo, wave_cap)
-            if not wave:
-                raise RuntimeError("KV cache too small for a single sequence")
-            for s, text in zip(wave, self._run_wave(wave)):
-                texts[s.idx] = text
-        return texts
+            seq = _Seq(0, p_ids, max(1, int(p.max_tokens)), float(p.temperature), base)
+            req = _Request(seq)
+            if len(p_ids) == 0 or len(p_ids) + seq.max_new > self.args.max_model_len or seq.max_new > OUT_WIDTH:
+                req.finish("")  # reference behaviour: the caller sees an unparsable (empty) output
+            reqs.append(req)
+        with self._cv:
+            self.stats["calls"] += 1
+            self._waiting.extend(r for r in reqs if not r.event.is_set())
+            self._cv.notify_all()
+        return reqs
 
-    def _admit(self, todo: List[_Seq], cap: int):
-        admitted, rest = [], []
-        for s in todo:
-            if len(admitted) >= cap:
-                rest.append(s)
-                continue
-            a = self.blocks.allocate(s.prompt_ids, s.max_new, self.args.prefix_caching)
-            if not a.ok:
-                rest.append(s)
-                continue
-            s.blocks, s.cached = list(a.blocks), a.num_cached_tokens
-            admitted.append(s)
-        return admitted, rest
+    def _device_ctx(self):
+        return torch.cuda.device(self.device) if self.device.type == "cuda" else contextlib.nullcontext()
 
-    def _block_table(self, wave: List[_Seq], rows: int) -> torch.Tensor:
+    # ---- background scheduler (continuous batching) ----
+    def start_async(self):
+        """Run the scheduler on a background thread; generate() then only enqueues + waits."""
+        if self.async_mode:
+            return
+        self.async_mode = True
+        self._stop = False
+        self._thread = threading.Thread(target=self._serve_forever, name="bcg-engine", daemon=True)
+        self._thread.start()
+
+    def _serve_forever(self):
+        with self._device_ctx():
+            while True:
+                with self._cv:
+                    while not self._stop and not self._waiting and not any(self.slots):
+                        self._cv.wait()
+                    if self._stop:
+                        return
+                try:
+                    self._iterate()
+                except BaseException as exc:  # fail every pending request loudly
+                    self._fail_all(exc)
+
+    def _fail_all(self, exc):
+        with self._cv:
+            pending = list(self._waiting)
+            self._waiting.clear()
+        for i, s in enumerate(self.slots):
+            if s is not None:
+                pending.append(s)
+                self.slots[i] = None
+        for r in pending:
+            r.exc = exc
+            r.event.set()
+
+    # ---- one scheduler iteration ----
+    def _iterate(self):
+        self._reap()
+        self._admit()
+        if any(self.slots):
+            self._decode_burst()
+
+    def _active_rows(self) -> List[int]:
+        return [i for i, r in enumerate(self.slots) if r is not None]
+
+    def _admit(self):
+        with self._cv:
+            if not self._waiting:
+                return
+            free = [i for i, r in enumerate(self.slots) if r is None]
+            cap = self.args.max_batch_seqs
+            if self.args.honor_max_num_seqs and self.args.max_num_seqs:
+                cap = min(cap, self.args.max_num_seqs)
+            budget = max(0, cap - (len(self.slots) - len(free)))
+            admitted = []
+            while self._waiting and free and len(admitted) < budget:
+                req = self._waiting[0]
+                a = self.blocks.allocate(req.seq.prompt_ids, req.seq.max_new, self.args.prefix_caching)
+                if not a.ok:
+                    break
+                self._waiting.popleft()
+                req.seq.blocks, req.seq.cached = list(a.blocks), a.num_cached_tokens
+                req.row = free.pop(0)
+                self.slots[req.row] = req
+                admitted.append(req)
+            if not admitted and not any(self.slots) and self._waiting:
+                raise RuntimeError("KV cache too small for a single waiting sequence")
+        if admitted:
+            self._start_sequences(admitted)
+
+    def _start_sequences(self, reqs: List["_Request"]):
+        """Write the new rows' state, prefill their prompts, sample their first tokens."""
+        st, dev = self.state, self.device
+        rows = torch.tensor([r.row for r in reqs], dtype=torch.long)
+        seqs = [r.seq for r in reqs]
+        table_cpu = self._block_table(seqs, len(seqs))
+        rows_d = rows.to(dev)
+        st["block_tables"].index_copy_(0, rows_d, table_cpu.to(dev))
+        vals = {"seq_lens": [len(s.prompt_ids) for s in seqs], "fsm_base": [s.fsm_base for s in seqs],
+                "fsm_state": [0] * len(seqs), "gen_count": [0] * len(seqs),
+                "max_new": [s.max_new for s in seqs], "row_keys": [self._next_key() for _ in seqs],
+                "done": [0] * len(seqs), "next_tokens": [0] * len(seqs)}
+        for key, v in vals.items():
+            st[key].index_copy_(0, rows_d, torch.tensor(v, dtype=torch.int32).to(dev))
+        st["temperature"].index_copy_(0, rows_d, torch.tensor([s.temperature for s in seqs],
+                                                               dtype=torch.float32).to(dev))
+        with self.timer.phase("prefill"):
+            logits = self._prefill(seqs, table_cpu)
+        for s in seqs:  # prompt blocks are now resident: make them reusable
+            self.blocks.commit_prompt(s.blocks, s.prompt_ids)
+            self.stats["prompt_tokens"] += len(s.prompt_ids)
+            self.stats["cached_tokens"] += s.cached
+        with self.timer.phase("sample"):
+            sub = {k: v.index_select(0, rows_d) for k, v in st.items() if k != "block_tables"}
+            self._sample(logits, sub)
+            for k, v in sub.items():
+                st[k].index_copy_(0, rows_d, v)
+
+    def _decode_burst(self):
+        """`poll_every` decode steps over the rows [0, bucket)."""
+        rows = self._active_rows()
+        n = rows[-1] + 1
+        with self.timer.phase("decode"):
+            steps = self.graphs.run_burst(n) if self.graphs is not None else self._eager_burst(n)
+        self.stats["decode_steps"] += steps
+
+    def _eager_burst(self, n: int) -> int:
+        view = {k: v[:n] for k, v in self.state.items()}
+        for _ in range(self.args.poll_every):
+            self.decode_step(view)
+        return self.args.poll_every
+
+    def _reap(self):
+        """Complete finished rows: detokenise, free KV blocks and slots, compact."""
+        rows = self._active_rows()
+        if not rows:
+            return
+        n = rows[-1] + 1
+        done = self.state["done"][:n].tolist()
+        finished = [i for i in rows if done[i]]
+        if not finished:
+            return
+        with self.timer.phase("detokenize"):
+            counts = self.state["gen_count"][:n].tolist()
+            idx = torch.tensor(finished, dtype=torch.long, device=self.device)
+            outs = self.state["out_tokens"].index_select(0, idx).tolist()
+            for i, toks in zip(finished, outs):
+                req = self.slots[i]
+                toks = toks[:counts[i]]
+                if req.seq.fsm_base < 0 and toks and toks[-1] in self.eos_ids:
+                    toks = toks[:-1]
+                self.stats["generated_tokens"] += counts[i]
+                text = self.tokenizer.decode_bytes(toks).decode("utf-8", errors="replace")
+                self.blocks.free(req.seq.blocks)
+                self.slots[i] = None
+                req.finish(text)
+        self._park_rows(finished)
+        self._compact()
+
+    def _park_rows(self, rows: List[int]):
+        """Inactive rows: done, context 1 on the scratch block (harmless in the graph)."""
+        if not rows:
+            return
+        idx = torch.tensor(rows, dtype=torch.long, device=self.device)
+        st = self.state
+        st["done"].index_fill_(0, idx, 1)
+        st["seq_lens"].index_fill_(0, idx, 1)
+        st["fsm_base"].index_fill_(0, idx, -1)
+        st["block_tables"].index_fill_(0, idx, 0)
+
+    def _compact(self):
+        """Move the highest live rows into free low slots when that shrinks the graph bucket."""
+        from .graphs import bucket_for
+        rows = self._active_rows()
+        if not rows:
+            return
+        if bucket_for(rows[-1] + 1) <= bucket_for(len(rows)):
+            return
+        free = [i for i in range(len(rows)) if self.slots[i] is None]
+        movers = [i for i in reversed(rows) if i >= len(rows)][:len(free)]
+        if not movers:
+            return
+        src = torch.tensor(movers, dtype=torch.long, device=self.device)
+        dst = torch.tensor(free[:len(movers)], dtype=torch.long, device=self.device)
+        for key, t in self.state.items():
+            t.index_copy_(0, dst, t.index_select(0, src))
+        for a, b in zip(movers, free):
+            self.slots[b], self.slots[a] = self.slots[a], None
+            self.slots[b].row = b
+        self._park_rows(movers)
+
+    def _block_table(self, seqs: List[_Seq], rows: int) -> torch.Tensor:
         t = torch.zeros(rows, self.max_blocks_per_seq, dtype=torch.int32)
-        for r, s in enumerate(wave):
+        for r, s in enumerate(seqs):
             phys = self._phys(s.blocks)
             t[r, :len(phys)] = torch.tensor(phys, dtype=torch.int32)
         return t
 
-    def _run_wave(self, wave: List[_Seq]) -> List[str]:
-        B = len(wave)
-        dev = self.device
-        bs = self.args.kv_block_size
-        max_new = max(s.max_new for s in wave)
-        table_cpu = self._block_table(wave, B)
-        st = {
-            "block_tables": table_cpu.to(dev),
-            "seq_lens": torch.tensor([len(s.prompt_ids) for s in wave], dtype=torch.int32, device=dev),
-            "fsm_base": torch.tensor([s.fsm_base for s in wave], dtype=torch.int32, device=dev),
-            "fsm_state": torch.zeros(B, dtype=torch.int32, device=dev),
-            "gen_count": torch.zeros(B, dtype=torch.int32, device=dev),
-            "max_new": torch.tensor([s.max_new for s in wave], dtype=torch.int32, device=dev),
-            "temperature": torch.tensor([s.temperature for s in wave], dtype=torch.float32, device=dev),
-            "row_keys": torch.tensor([self._next_key() for _ in wave], dtype=torch.int32, device=dev),
-            "done": torch.zeros(B, dtype=torch.int32, device=dev),
-            "next_tokens": torch.zeros(B, dtype=torch.int32, device=dev),
-            "out_tokens": torch.zeros(B, max_new, dtype=torch.int32, device=dev),
-        }
-        with self.timer.phase("prefill"):
-            logits = self._prefill(wave, table_cpu, st["block_tables"])
-        for s in wave:  # prompt blocks are now resident: make them reusable
-            self.blocks.commit_prompt(s.blocks, s.prompt_ids)
-        with self.timer.phase("sample"):
-            self._sample(logits, st)
-        with self.timer.phase("decode"):
-            self._decode(st, B, max_new)
-        with self.timer.phase("detokenize"):
-            counts = st["gen_count"].cpu().tolist()
-            outs = st["out_tokens"].cpu().tolist()
-            texts = []
-            for r, s in enumerate(wave):
-                toks = outs[r][:counts[r]]
-                if s.fsm_base < 0 and toks and toks[-1] in self.eos_ids:
-                    toks = toks[:-1]
-                self.stats["generated_tokens"] += counts[r]
-                texts.append(self.tokenizer.decode_bytes(toks).decode("utf-8", errors="replace"))
-        for s in wave:
-            self.blocks.free(s.blocks)
-            self.stats["prompt_tokens"] += len(s.prompt_ids)
-            self.stats["cached_tokens"] += s.cached
-        return texts
-
     def _next_key(self) -> int:
         self._req_counter += 1
-        x = (self._req_counter * 0x9E3779B1 + self.seed) & 0x7FFFFFFF
-        return x
+        return (self._req_counter * 0x9E3779B1 + self.seed) & 0x7FFFFFFF
 
     # ------------------------------------------------------------- prefill
-    def _prefill(self, wave: List[_Seq], table_cpu: torch.Tensor, table_dev: torch.Tensor) -> torch.Tensor:
+    def _prefill(self, wave: List[_Seq], table_cpu: torch.Tensor) -> torch.Tensor:
         """Chunked packed prefill; returns last-token logits ``[B, V]``."""
-        dev, bs = self.device, self.args.kv_block_size
+        dev = self.device
         V = self.model.cfg.vocab_size
         logits_out = torch.empty(len(wave), V, dtype=self.args.dtype, device=dev)
         budget = self.args.prefill_chunk_tokens
-        # (row, start, end) segments of uncached prompt tokens
-        segments = []
+        segments = []  # (row, start, end) of uncached prompt tokens
         for r, s in enumerate(wave):
             pos, n = s.cached, len(s.prompt_ids)
             while pos < n:
@@ -333,7 +477,6 @@ class InferenceEngine:
                 self._prefill_chunk(wave, chunk, table_cpu, logits_out)
             chunk, used = ([seg], seg[2] - seg[1]) if seg is not None else ([], 0)
         return logits_out
-
     def _prefill_chunk(self, wave, chunk, table_cpu, logits_out):
         dev, bs = self.device, self.args.kv_block_size
         toks, pos, slots, q_start, seq_lens, rows, last_idx, last_rows = [], [], [], [0], [], [], [], []
@@ -393,20 +536,25 @@ class InferenceEngine:
         logits = self.model.forward(st["next_tokens"], self.decode_meta(st), self.k_cache, self.v_cache)
         self._sample(logits, st)
 
-    def _decode(self, st: Dict[str, torch.Tensor], B: int, max_new: int):
-        steps = 0
-        if self.graphs is not None:
-            steps = self.graphs.run(st, B, max_new)
-        else:
-            poll = self.args.poll_every
-            for i in range(1, max_new):
-                if i % poll == 1 and bool(st["done"].all()):
-                    break
-                self.decode_step(st)
-                steps += 1
-        self.stats["decode_steps"] += steps
-
     def shutdown(self):
+        if self.async_mode:
+            with self._cv:
+                self._stop = True
+                self._cv.notify_all()
+            self._thread.join(timeout=30)
+            self.async_mode = False
         self.graphs = None
         self.k_cache = self.v_cache = None
         self.model = None
+
+
+class _Request:
+    __slots__ = ("seq", "row", "text", "exc", "event")
+
+    def __init__(self, seq: _Seq):
+        self.seq, self.row, self.text, self.exc = seq, -1, "", None
+        self.event = threading.Event()
+
+    def finish(self, text: str):
+        self.text = text
+        self.event.set()

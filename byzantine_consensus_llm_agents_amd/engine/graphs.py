@@ -1,13 +1,15 @@
 """HIP-graph capture of the full decode step (forward + guided sampling).
 
-One graph per batch bucket.  A decode step launches ~10 kernels per layer
-(GEMMs, norm, rope/KV-write, attention + combine, SiLU, all-reduce under TP)
-plus the sampler -- ~400 launches for Qwen3-14B -- so eager launching would
-be host-bound; a replay costs one ``hipGraphLaunch``.  All per-row state lives
-in static device buffers, the sampler advances it in place, and the host
-only polls the ``done`` flags every ``poll_every`` replays.
+A decode step launches ~10 kernels per layer (GEMMs, norms, rope/KV-write,
+attention + split combine, SiLU, all-reduce under TP) plus the sampler --
+~400 launches for Qwen3-14B -- so eager launching is host-bound; a replay
+costs one ``hipGraphLaunch``.
 
-Padding rows of a bucket are marked done and point at the scratch KV block 0.
+All graphs read and write the engine's single per-row state table
+(``engine.state``): the graph of bucket ``b`` is captured over the views
+``state[k][:b]``, so every bucket sees the same rows and the continuous-batching
+scheduler can admit / retire / compact rows between bursts of replays without
+re-capturing.  Inactive rows are parked (done, context 1 on scratch block 0).
 Graphs are invalidated when the FSM table is re-allocated (its pointer is
 baked into the captured sampler launch).
 """
@@ -17,93 +19,59 @@ from typing import Dict
 import torch
 
 BUCKETS = (1, 2, 4, 8, 12, 16, 24, 32, 40, 48, 64, 80, 96, 128, 160, 192, 224, 256, 320, 384, 448, 512)
-OUT_WIDTH = 1024  # max tokens per sequence handled by the graph path
+MAX_ROWS = BUCKETS[-1]
+
+
+def bucket_for(n: int) -> int:
+    for b in BUCKETS:
+        if b >= n:
+            return b
+    return MAX_ROWS
 
 
 class DecodeGraphs:
     def __init__(self, engine):
         self.engine = engine
-        self.graphs: Dict[int, tuple] = {}
+        self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.pool = None
         self.version = None
         self.captures = 0
 
-    def _bucket(self, B: int) -> int:
-        for b in BUCKETS:
-            if b >= B:
-                return b
-        return -1
+    def _views(self, b: int):
+        return {k: v[:b] for k, v in self.engine.state.items()}
 
-    def _static(self, Bb: int) -> Dict[str, torch.Tensor]:
+    def _capture(self, b: int) -> torch.cuda.CUDAGraph:
         e = self.engine
-        dev = e.device
-        z = lambda: torch.zeros(Bb, dtype=torch.int32, device=dev)  # noqa: E731
-        st = {"block_tables": torch.zeros(Bb, e.max_blocks_per_seq, dtype=torch.int32, device=dev),
-              "seq_lens": torch.ones(Bb, dtype=torch.int32, device=dev),
-              "fsm_base": torch.full((Bb,), -1, dtype=torch.int32, device=dev),
-              "fsm_state": z(), "gen_count": z(), "max_new": torch.ones(Bb, dtype=torch.int32, device=dev),
-              "temperature": torch.zeros(Bb, dtype=torch.float32, device=dev), "row_keys": z(),
-              "done": torch.ones(Bb, dtype=torch.int32, device=dev), "next_tokens": z(),
-              "out_tokens": torch.zeros(Bb, OUT_WIDTH, dtype=torch.int32, device=dev)}
-        return st
-
-    def _capture(self, Bb: int):
-        e = self.engine
-        st = self._static(Bb)
+        view = self._views(b)
+        # capture-time replays must not disturb live rows: snapshot the state
+        saved = {k: v.clone() for k, v in e.state.items()}
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(2):  # warm-up: allocator + library plans
-                e.decode_step(st)
+                e.decode_step(view)
         torch.cuda.current_stream().wait_stream(side)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, pool=self.pool):
-            e.decode_step(st)
+            e.decode_step(view)
+        for k, v in e.state.items():
+            v.copy_(saved[k])
         torch.cuda.synchronize()
         self.captures += 1
-        return graph, st
+        return graph
 
-    def run(self, st: Dict[str, torch.Tensor], B: int, max_new: int) -> int:
+    def run_burst(self, n_rows: int) -> int:
+        """Replay the bucket covering rows [0, n_rows) `poll_every` times."""
         e = self.engine
-        Bb = self._bucket(B)
-        if Bb < 0 or max_new > OUT_WIDTH:
-            return self._eager(st, max_new)
         if self.version != e.fsm.version:
             self.graphs.clear()
             self.version = e.fsm.version
-        if Bb not in self.graphs:
-            self.graphs[Bb] = self._capture(Bb)
-        graph, s = self.graphs[Bb]
-        # load this wave into the static buffers (rows >= B stay padding)
-        s["done"].fill_(1)
-        s["seq_lens"].fill_(1)
-        s["block_tables"].zero_()
-        s["fsm_base"].fill_(-1)
-        for key in ("block_tables", "seq_lens", "fsm_base", "fsm_state", "gen_count", "max_new",
-                    "temperature", "row_keys", "done", "next_tokens"):
-            s[key][:B].copy_(st[key])
-        s["out_tokens"][:B, :max_new].copy_(st["out_tokens"])
-        done_view = s["done"][:B]
-        poll = e.args.poll_every
-        steps = 0
-        for i in range(1, max_new):
-            if i % poll == 1 and bool(done_view.all()):
-                break
+        b = bucket_for(n_rows)
+        graph = self.graphs.get(b)
+        if graph is None:
+            graph = self.graphs[b] = self._capture(b)
+        for _ in range(e.args.poll_every):
             graph.replay()
-            steps += 1
-        for key in ("gen_count", "done", "seq_lens", "fsm_state"):
-            st[key].copy_(s[key][:B])
-        st["out_tokens"].copy_(s["out_tokens"][:B, :max_new])
-        return steps
-
-    def _eager(self, st, max_new: int) -> int:
-        e = self.engine
-        steps = 0
-        for i in range(1, max_new):
-            if i % e.args.poll_every == 1 and bool(st["done"].all()):
-                break
-            e.decode_step(st)
-            steps += 1
-        return steps
+        return e.args.poll_every

@@ -11,10 +11,13 @@ Backends:
   * ``torch`` - the same engine on PyTorch reference ops (CPU tests);
   * ``fake``  - scripted schema-valid answers (plumbing, parity tests).
 
-Several simulations may share one ``LLM`` from different threads: calls are
-coalesced (:class:`Coalescer`) into a single device batch once every
-registered simulation is waiting on the engine, which is how one GPU serves
-many independent BCG seeds per batched round.
+Several simulations may share one ``LLM`` from different threads.  With
+``start_continuous_batching()`` (TP = 1) every call's sequences join the
+engine's running decode batch as soon as they arrive and leave it when they
+finish (iteration-level scheduling).  Otherwise calls are coalesced
+(:class:`Coalescer`) into one batch once every registered thread waits on the
+engine -- deterministic batch composition, required when TP ranks must make
+identical scheduling decisions.
 """
 
 import os
@@ -87,6 +90,8 @@ class Coalescer:
             self._cond.notify_all()
 
     def _flush(self, tickets):
+        # deterministic row order (TP ranks must build identical batches)
+        tickets = sorted(tickets, key=lambda t: t["key"])
         prompts, params, spans = [], [], []
         for t in tickets:
             spans.append((len(prompts), len(t["prompts"])))
@@ -103,7 +108,8 @@ class Coalescer:
             t["done"] = True
 
     def submit(self, prompts, params):
-        ticket = {"prompts": prompts, "params": params, "done": False}
+        key = getattr(threading.current_thread(), "_bcg_order_key", ())
+        ticket = {"prompts": prompts, "params": params, "done": False, "key": key}
         with self._cond:
             self._tickets.append(ticket)
             self._maybe_flush_locked()
@@ -190,12 +196,21 @@ class LLM:
                 raise ValueError("need one SamplingParams per prompt")
         if not prompts:
             return []
-        texts = self.coalescer.submit(prompts, params)
+        if getattr(self.backend, "async_mode", False):
+            # continuous batching: requests join the running batch directly
+            texts = self._run_batch(prompts, params)
+        else:
+            texts = self.coalescer.submit(prompts, params)
         outs = []
         for p, t in zip(prompts, texts):
             outs.append(RequestOutput(self._next_id, p, [CompletionOutput(0, t)]))
             self._next_id += 1
         return outs
+
+    def start_continuous_batching(self):
+        """Switch the engine to its background scheduler (DP / TP=1 serving)."""
+        if hasattr(self.backend, "start_async"):
+            self.backend.start_async()
 
     def shutdown(self):
         self.backend.shutdown()

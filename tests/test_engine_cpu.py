@@ -1,0 +1,77 @@
+"""Engine on the torch backend (CPU): guided JSON, heterogeneous schemas, continuous batching."""
+import json
+import threading
+
+import pytest
+
+from byzantine_consensus_llm_agents_amd.bcg import prompts as P
+
+
+@pytest.fixture(scope="module")
+def llm():
+    from byzantine_consensus_llm_agents_amd.bcg.config import ENGINE_CONFIG
+    from byzantine_consensus_llm_agents_amd.engine import LLM
+    ENGINE_CONFIG["budget_aware_json"] = True
+    eng = LLM("bcg/tiny-qwen3", backend="torch", seed=3, max_model_len=1024, kv_cache_gb=0.25,
+              max_batch_seqs=12)
+    yield eng
+    eng.shutdown()
+    ENGINE_CONFIG["budget_aware_json"] = False
+
+
+SCHEMAS = [P.honest_decision_schema(0, 50), P.byzantine_decision_schema(0, 50),
+           P.vote_schema(P.HONEST_VOTE_OPTIONS), P.vote_schema(P.BYZANTINE_VOTE_OPTIONS)]
+
+
+def _params(i, max_tokens=24):
+    """Decide schemas need ~15+ tokens for their shortest JSON, votes ~6."""
+    from byzantine_consensus_llm_agents_amd.engine import GuidedDecodingParams, SamplingParams
+    if i % 4 < 2:
+        max_tokens += 32
+    return SamplingParams(temperature=[0.0, 0.5][i % 2], max_tokens=max_tokens,
+                          guided_decoding=GuidedDecodingParams(json=SCHEMAS[i % 4]))
+
+
+def _check(outs, params):
+    for o, p in zip(outs, params):
+        obj = json.loads(o.outputs[0].text)
+        sch = p.guided_decoding.json
+        assert set(sch["required"]) <= set(obj) <= set(sch["properties"])
+
+
+def test_sync_heterogeneous_batch(llm):
+    prompts = [f"<|im_start|>user\nagent_{i} round {i}<|im_end|>\n<|im_start|>assistant\n" for i in range(8)]
+    params = [_params(i) for i in range(8)]
+    outs = llm.generate(prompts, params)
+    _check(outs, params)
+    assert llm.backend.stats["calls"] >= 1
+
+
+def test_more_requests_than_rows_and_prefix_cache(llm):
+    # 20 sequences through 12 rows: admission waits for rows, compaction reuses them
+    base = "<|im_start|>system\n" + "You are a careful consensus agent. " * 8 + "<|im_end|>\n"
+    prompts = [base + f"<|im_start|>user\nround {i}<|im_end|>\n<|im_start|>assistant\n" for i in range(20)]
+    params = [_params(i, max_tokens=[8, 24, 16][i % 3]) for i in range(20)]
+    before = llm.backend.stats["cached_tokens"]
+    _check(llm.generate(prompts, params), params)
+    _check(llm.generate(prompts[:4], params[:4]), params[:4])
+    assert llm.backend.stats["cached_tokens"] > before
+
+
+def test_continuous_batching_threads(llm):
+    llm.start_continuous_batching()
+    results = {}
+
+    def client(k):
+        prompts = [f"<|im_start|>user\nclient {k} msg {j}<|im_end|>\n<|im_start|>assistant\n" for j in range(3)]
+        params = [_params(k + j, max_tokens=8 + 4 * j) for j in range(3)]
+        results[k] = (llm.generate(prompts, params), params)
+
+    threads = [threading.Thread(target=client, args=(k,)) for k in range(5)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=600)
+    assert len(results) == 5
+    for outs, params in results.values():
+        _check(outs, params)
