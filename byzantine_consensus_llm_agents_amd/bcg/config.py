@@ -89,7 +89,7 @@ ENGINE_CONFIG = {
     "max_whitespace": 4,           # JSON grammar: max consecutive whitespace chars
     "prefix_caching": True,
     "use_hip_graphs": True,
-    "max_batch_seqs": 512,
+    "max_batch_seqs": 768,
     "prefill_chunk_tokens": 16384,
     "honor_max_num_seqs": False,
     "kv_cache_gb": None,           # None = size from gpu_memory_utilization

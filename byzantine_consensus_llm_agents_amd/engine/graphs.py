@@ -18,7 +18,8 @@ from typing import Dict
 
 import torch
 
-BUCKETS = (1, 2, 4, 8, 12, 16, 24, 32, 40, 48, 64, 80, 96, 128, 160, 192, 224, 256, 320, 384, 448, 512)
+BUCKETS = (1, 2, 4, 8, 12, 16, 24, 32, 40, 48, 64, 80, 96, 128, 160, 192, 224, 256, 320, 384, 448, 512,
+           640, 768)
 MAX_ROWS = BUCKETS[-1]
 
 
