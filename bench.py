@@ -126,8 +126,19 @@ class SimPool:
         return sum(made)
 
 
+def _heartbeat(llm, stop: threading.Event, every: float = 30.0):
+    """Progress line on stderr every `every` s (long runs must keep writing)."""
+    t0 = time.perf_counter()
+    while not stop.wait(every):
+        st = dict(getattr(llm.backend, "stats", {}))
+        print(f"[progress] {time.perf_counter() - t0:.0f}s {json.dumps(st)}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
+    if os.environ.get("BCG_STACKS_AFTER"):  # debugging aid: dump every thread's stack periodically
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["BCG_STACKS_AFTER"]), repeat=True, file=sys.stderr)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -160,6 +171,9 @@ def main():
     EngineAgent._shared_model_config = dict(C.VLLM_CONFIG)
     init_s = time.perf_counter() - t0
 
+    stop_hb = threading.Event()
+    if rank == 0:
+        threading.Thread(target=_heartbeat, args=(llm, stop_hb), daemon=True).start()
     lockstep = args.tp > 1  # TP ranks need identical batches: coalesced lock-step rounds
     if not lockstep:
         llm.start_continuous_batching()
@@ -167,7 +181,7 @@ def main():
                    args.seed + rank // args.tp, rank // args.tp)
     if args.warmup:
         n = pool.run(args.warmup, llm, lockstep)
-        if rank == 0 and args.verbose:
+        if rank == 0:
             print(f"[warmup] {args.warmup} rounds/sim, decisions={n}", file=sys.stderr, flush=True)
 
     eng = getattr(llm.backend, "stats", {})
@@ -223,6 +237,7 @@ def main():
                        "phases_rank0": llm.backend.timer.summary() if hasattr(llm.backend, "timer") else {}},
         }
         print(json.dumps(line), flush=True)
+    stop_hb.set()
     llm.shutdown()
     if world > 1:
         dist.destroy_process_group()

@@ -93,4 +93,9 @@ ENGINE_CONFIG = {
     "prefill_chunk_tokens": 16384,
     "honor_max_num_seqs": False,
     "kv_cache_gb": None,           # None = size from gpu_memory_utilization
+    # prefill on a second HIP stream, overlapped with decode bursts (single-GPU / DP ranks).
+    # Off by default: measured no gain at 32 sims/GPU (19.2 vs 19.1 decisions/s), and
+    # hipBLASLt's stream-K prefill GEMMs (inter-workgroup waits) beside a second
+    # persistent kernel can starve each other -- one run hung.
+    "overlap_prefill": os.environ.get("BCG_OVERLAP_PREFILL", "0") == "1",
 }

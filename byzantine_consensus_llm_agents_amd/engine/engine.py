@@ -65,6 +65,7 @@ class EngineArgs:
     device: Optional[str] = None
     poll_every: int = 8
     async_mode: bool = False
+    overlap_prefill: bool = False  # prefill on its own HIP stream, concurrent with decode bursts
 
     @classmethod
     def from_configs(cls, model: str, backend: str, weights: Optional[str] = None,
@@ -83,7 +84,8 @@ class EngineArgs:
                    prefix_caching=ec.get("prefix_caching", True),
                    use_hip_graphs=ec.get("use_hip_graphs", True),
                    kv_cache_gb=ec.get("kv_cache_gb"),
-                   honor_max_num_seqs=ec.get("honor_max_num_seqs", False))
+                   honor_max_num_seqs=ec.get("honor_max_num_seqs", False),
+                   overlap_prefill=ec.get("overlap_prefill", False))
         dtype = ec.get("dtype", "bfloat16")
         args.dtype = getattr(torch, dtype) if isinstance(dtype, str) else dtype
         for key, value in kw.items():
@@ -149,6 +151,12 @@ class InferenceEngine:
         self._waiting: Deque[_Request] = collections.deque()
         self.async_mode = False
         self.graphs = None
+        # Prefill (MFMA-bound GEMMs) runs on a second stream while decode bursts
+        # (HBM-bound) keep replaying on the main stream.  Off under TP: RCCL
+        # collectives of one communicator must not run on two streams at once.
+        self.overlap = bool(args.overlap_prefill and self.device.type == "cuda" and self.tp.size == 1)
+        self.prefill_stream = torch.cuda.Stream(self.device) if self.overlap else None
+        self._inflight = None
         if self.backend == "hip" and args.use_hip_graphs:
             from .graphs import DecodeGraphs
             self.graphs = DecodeGraphs(self)
@@ -295,6 +303,7 @@ class InferenceEngine:
                     self._fail_all(exc)
 
     def _fail_all(self, exc):
+        self._inflight = None
         with self._cv:
             pending = list(self._waiting)
             self._waiting.clear()
@@ -309,12 +318,20 @@ class InferenceEngine:
     # ---- one scheduler iteration ----
     def _iterate(self):
         self._reap()
-        self._admit()
-        if any(self.slots):
+        if self._inflight is not None and (not self._live_rows() or self._inflight["event"].query()):
+            self._finish_prefill()
+        if self._inflight is None:
+            self._admit()
+        if self._live_rows():
             self._decode_burst()
 
     def _active_rows(self) -> List[int]:
+        """Occupied rows (decoding, or pending: prefill in flight)."""
         return [i for i, r in enumerate(self.slots) if r is not None]
+
+    def _live_rows(self) -> List[int]:
+        """Rows the decode graphs advance (prefill done)."""
+        return [i for i, r in enumerate(self.slots) if r is not None and not r.pending]
 
     def _admit(self):
         with self._cv:
@@ -334,21 +351,47 @@ class InferenceEngine:
                 self._waiting.popleft()
                 req.seq.blocks, req.seq.cached = list(a.blocks), a.num_cached_tokens
                 req.row = free.pop(0)
+                req.pending = True
                 self.slots[req.row] = req
                 admitted.append(req)
             if not admitted and not any(self.slots) and self._waiting:
                 raise RuntimeError("KV cache too small for a single waiting sequence")
         if admitted:
-            self._start_sequences(admitted)
+            self._launch_prefill(admitted)
+            if not self.overlap:
+                self._finish_prefill()
 
-    def _start_sequences(self, reqs: List["_Request"]):
-        """Write the new rows' state, prefill their prompts, sample their first tokens."""
-        st, dev = self.state, self.device
-        rows = torch.tensor([r.row for r in reqs], dtype=torch.long)
+    def _launch_prefill(self, reqs: List["_Request"]):
+        """Enqueue the prompts' prefill; with overlap on the prefill stream, without blocking the host.
+
+        The new rows stay parked (done, scratch block) in the decode state until
+        `_finish_prefill`, so bursts replayed meanwhile leave them untouched.
+        """
         seqs = [r.seq for r in reqs]
         table_cpu = self._block_table(seqs, len(seqs))
-        rows_d = rows.to(dev)
-        st["block_tables"].index_copy_(0, rows_d, table_cpu.to(dev))
+        stream = self.prefill_stream
+        ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+        if stream is not None:
+            stream.wait_stream(torch.cuda.current_stream())
+        with self.timer.phase("prefill"), ctx:
+            plans = self._plan_prefill(seqs, table_cpu)
+            logits = self._run_prefill(plans, len(seqs))
+            event = torch.cuda.Event() if stream is not None else None
+            if event is not None:
+                event.record(stream)
+        self._inflight = {"reqs": reqs, "table": table_cpu, "logits": logits, "event": event}
+
+    def _finish_prefill(self):
+        """Activate the in-flight wave: write its state rows, commit prompt blocks, sample token 1."""
+        fl, self._inflight = self._inflight, None
+        reqs, logits = fl["reqs"], fl["logits"]
+        if fl["event"] is not None:
+            torch.cuda.current_stream().wait_event(fl["event"])
+            logits.record_stream(torch.cuda.current_stream())
+        st, dev = self.state, self.device
+        seqs = [r.seq for r in reqs]
+        rows_d = torch.tensor([r.row for r in reqs], dtype=torch.long).to(dev)
+        st["block_tables"].index_copy_(0, rows_d, fl["table"].to(dev))
         vals = {"seq_lens": [len(s.prompt_ids) for s in seqs], "fsm_base": [s.fsm_base for s in seqs],
                 "fsm_state": [0] * len(seqs), "gen_count": [0] * len(seqs),
                 "max_new": [s.max_new for s in seqs], "row_keys": [self._next_key() for _ in seqs],
@@ -357,8 +400,6 @@ class InferenceEngine:
             st[key].index_copy_(0, rows_d, torch.tensor(v, dtype=torch.int32).to(dev))
         st["temperature"].index_copy_(0, rows_d, torch.tensor([s.temperature for s in seqs],
                                                                dtype=torch.float32).to(dev))
-        with self.timer.phase("prefill"):
-            logits = self._prefill(seqs, table_cpu)
         for s in seqs:  # prompt blocks are now resident: make them reusable
             self.blocks.commit_prompt(s.blocks, s.prompt_ids)
             self.stats["prompt_tokens"] += len(s.prompt_ids)
@@ -368,10 +409,12 @@ class InferenceEngine:
             self._sample(logits, sub)
             for k, v in sub.items():
                 st[k].index_copy_(0, rows_d, v)
+        for r in reqs:
+            r.pending = False
 
     def _decode_burst(self):
         """`poll_every` decode steps over the rows [0, bucket)."""
-        rows = self._active_rows()
+        rows = self._live_rows()
         n = rows[-1] + 1
         with self.timer.phase("decode"):
             steps = self.graphs.run_burst(n) if self.graphs is not None else self._eager_burst(n)
@@ -385,7 +428,7 @@ class InferenceEngine:
 
     def _reap(self):
         """Complete finished rows: detokenise, free KV blocks and slots, compact."""
-        rows = self._active_rows()
+        rows = self._live_rows()
         if not rows:
             return
         n = rows[-1] + 1
@@ -422,15 +465,19 @@ class InferenceEngine:
         st["block_tables"].index_fill_(0, idx, 0)
 
     def _compact(self):
-        """Move the highest live rows into free low slots when that shrinks the graph bucket."""
+        """Move the highest live rows into free low slots when that shrinks the graph bucket.
+
+        Pending rows (prefill in flight) never move: their state is written on activation.
+        """
         from .graphs import bucket_for
-        rows = self._active_rows()
-        if not rows:
+        occupied = self._active_rows()
+        live = self._live_rows()
+        if not live:
             return
-        if bucket_for(rows[-1] + 1) <= bucket_for(len(rows)):
+        if bucket_for(live[-1] + 1) <= bucket_for(len(occupied)):
             return
-        free = [i for i in range(len(rows)) if self.slots[i] is None]
-        movers = [i for i in reversed(rows) if i >= len(rows)][:len(free)]
+        free = [i for i in range(len(occupied)) if self.slots[i] is None]
+        movers = [i for i in reversed(live) if i >= len(occupied)][:len(free)]
         if not movers:
             return
         src = torch.tensor(movers, dtype=torch.long, device=self.device)
@@ -454,11 +501,14 @@ class InferenceEngine:
         return (self._req_counter * 0x9E3779B1 + self.seed) & 0x7FFFFFFF
 
     # ------------------------------------------------------------- prefill
-    def _prefill(self, wave: List[_Seq], table_cpu: torch.Tensor) -> torch.Tensor:
-        """Chunked packed prefill; returns last-token logits ``[B, V]``."""
-        dev = self.device
-        V = self.model.cfg.vocab_size
-        logits_out = torch.empty(len(wave), V, dtype=self.args.dtype, device=dev)
+    def _h2d(self, t: torch.Tensor) -> torch.Tensor:
+        """Host->device copy that never blocks the host (pinned staging, async on the current stream)."""
+        if self.device.type != "cuda":
+            return t
+        return t.pin_memory().to(self.device, non_blocking=True)
+
+    def _plan_prefill(self, wave: List[_Seq], table_cpu: torch.Tensor) -> List[tuple]:
+        """Split the uncached prompt tokens into packed chunks; upload every chunk's metadata first."""
         budget = self.args.prefill_chunk_tokens
         segments = []  # (row, start, end) of uncached prompt tokens
         for r, s in enumerate(wave):
@@ -467,18 +517,19 @@ class InferenceEngine:
                 end = min(n, pos + budget)
                 segments.append((r, pos, end))
                 pos = end
-        chunk, used = [], 0
+        plans, chunk, used = [], [], 0
         for seg in segments + [None]:
             if seg is not None and used + (seg[2] - seg[1]) <= budget:
                 chunk.append(seg)
                 used += seg[2] - seg[1]
                 continue
             if chunk:
-                self._prefill_chunk(wave, chunk, table_cpu, logits_out)
+                plans.append(self._plan_chunk(wave, chunk, table_cpu))
             chunk, used = ([seg], seg[2] - seg[1]) if seg is not None else ([], 0)
-        return logits_out
-    def _prefill_chunk(self, wave, chunk, table_cpu, logits_out):
-        dev, bs = self.device, self.args.kv_block_size
+        return plans
+
+    def _plan_chunk(self, wave, chunk, table_cpu):
+        bs = self.args.kv_block_size
         toks, pos, slots, q_start, seq_lens, rows, last_idx, last_rows = [], [], [], [0], [], [], [], []
         for r, a, b in chunk:
             s = wave[r]
@@ -499,21 +550,30 @@ class InferenceEngine:
             for t in range(q_start[i], q_start[i + 1], 64):
                 tiles.append((b - (q_start[i + 1] - t), i, t, min(t + 64, q_start[i + 1])))
         tiles.sort(key=lambda x: -x[0])
+        i32 = torch.int32
         meta = AttnMeta(
-            tiles=torch.tensor([x[1:] for x in tiles], dtype=torch.int32, device=dev),
-            positions=torch.cat(pos).to(torch.int32).to(dev),
-            slots=torch.cat(slots).to(torch.int32).to(dev),
-            block_tables=table_cpu[rows].to(dev),
-            seq_lens=torch.tensor(seq_lens, dtype=torch.int32, device=dev),
-            q_start=torch.tensor(q_start, dtype=torch.int32, device=dev),
+            tiles=self._h2d(torch.tensor([x[1:] for x in tiles], dtype=i32)),
+            positions=self._h2d(torch.cat(pos).to(i32)),
+            slots=self._h2d(torch.cat(slots).to(i32)),
+            block_tables=self._h2d(table_cpu[rows]),
+            seq_lens=self._h2d(torch.tensor(seq_lens, dtype=i32)),
+            q_start=self._h2d(torch.tensor(q_start, dtype=i32)),
             max_q_len=max(b - a for _, a, b in chunk),
             decode=False,
-            logits_idx=torch.tensor(last_idx if last_idx else [0], dtype=torch.int64, device=dev))
-        tokens = torch.tensor(toks, dtype=torch.int32, device=dev)
-        logits = self.model.forward(tokens, meta, self.k_cache, self.v_cache)
-        if last_rows:
-            logits_out[torch.tensor(last_rows, device=dev)] = logits[:len(last_rows)].to(logits_out.dtype)
-        self.stats["prefill_chunks"] += 1
+            logits_idx=self._h2d(torch.tensor(last_idx if last_idx else [0], dtype=torch.int64)))
+        tokens = self._h2d(torch.tensor(toks, dtype=i32))
+        dest = self._h2d(torch.tensor(last_rows, dtype=torch.int64)) if last_rows else None
+        return tokens, meta, dest, len(last_rows)
+
+    def _run_prefill(self, plans, n_rows: int) -> torch.Tensor:
+        """Chunked packed prefill; returns last-token logits ``[n_rows, V]``."""
+        logits_out = torch.empty(n_rows, self.model.cfg.vocab_size, dtype=self.args.dtype, device=self.device)
+        for tokens, meta, dest, n_last in plans:
+            logits = self.model.forward(tokens, meta, self.k_cache, self.v_cache)
+            if n_last:
+                logits_out.index_copy_(0, dest, logits[:n_last].to(logits_out.dtype))
+            self.stats["prefill_chunks"] += 1
+        return logits_out
 
     # -------------------------------------------------------------- decode
     def _sample(self, logits: torch.Tensor, st: Dict[str, torch.Tensor]):
@@ -549,10 +609,10 @@ class InferenceEngine:
 
 
 class _Request:
-    __slots__ = ("seq", "row", "text", "exc", "event")
+    __slots__ = ("seq", "row", "text", "exc", "event", "pending")
 
     def __init__(self, seq: _Seq):
-        self.seq, self.row, self.text, self.exc = seq, -1, "", None
+        self.seq, self.row, self.text, self.exc, self.pending = seq, -1, "", None, False
         self.event = threading.Event()
 
     def finish(self, text: str):

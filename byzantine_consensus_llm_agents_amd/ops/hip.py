@@ -42,6 +42,9 @@ def load_library(path: str = None) -> ctypes.CDLL:
                                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                                         c_void_p, c_void_p],
         "bcg_decode_split_tokens": [c_int, c_int, c_int],
+        "bcg_paged_attention_decode_exp": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
+                                           c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int, c_int,
+                                           c_void_p, c_int, c_void_p],
         "bcg_gemm_skinny": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                             c_void_p],
         "bcg_guided_sample": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -118,21 +121,33 @@ def hip_ops() -> SimpleNamespace:
             n_q, n_kv, head_dim, NB, BS, eps, _stream()), "qk_norm_rope_kv_write")
         return q
 
-    _split_override = int(os.environ.get("BCG_DECODE_SPLIT", "0"))
-
     def paged_attention_decode(q, k_cache, v_cache, layer, block_tables, seq_lens, scale):
         B, n_q, hd = q.shape
         L, NB, n_kv, BS, _ = k_cache.shape
         _req(q.is_contiguous() and block_tables.dtype == torch.int32 and block_tables.is_contiguous()
              and block_tables.shape[0] == B and seq_lens.numel() == B, "decode attention inputs")
         max_blocks = block_tables.shape[1]
-        split = _split_override or lib.bcg_decode_split_tokens(B, n_kv, max_blocks * BS)
+        _req(B <= 1024, "decode attention: at most 1024 rows")
+        split = lib.bcg_decode_split_tokens(B, n_kv, max_blocks * BS)
         max_splits = (max_blocks * BS + split - 1) // split
         ws = torch.empty(B * n_q * max_splits * (hd + 2), dtype=torch.float32, device=q.device)
         out = torch.empty(B, n_q * hd, dtype=q.dtype, device=q.device)
         _check(lib.bcg_paged_attention_decode(
             _p(q), _p(k_cache), _p(v_cache), layer, NB, n_kv, _p(block_tables), max_blocks, _p(seq_lens),
             B, n_q, hd, BS, scale, _p(ws), max_splits, split, _p(out), _stream()), "paged_attention_decode")
+        return out
+
+    def paged_attention_decode_exp(q, k_cache, v_cache, layer, block_tables, seq_lens, scale, variant):
+        """Timing-only kernel variants (tools/bench_ops.py); not numerically valid for the engine."""
+        B, n_q, hd = q.shape
+        L, NB, n_kv, BS, _ = k_cache.shape
+        max_blocks = block_tables.shape[1]
+        max_splits = (max_blocks * BS + 127) // 128
+        ws = torch.empty(B * n_q * max_splits * (hd + 2), dtype=torch.float32, device=q.device)
+        out = torch.empty(B, n_q * hd, dtype=q.dtype, device=q.device)
+        _check(lib.bcg_paged_attention_decode_exp(
+            _p(q), _p(k_cache), _p(v_cache), layer, NB, n_kv, _p(block_tables), max_blocks, _p(seq_lens),
+            B, n_q, hd, scale, _p(ws), max_splits, 128, _p(out), variant, _stream()), "decode_exp")
         return out
 
     def paged_attention_prefill(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale,
@@ -194,5 +209,6 @@ def hip_ops() -> SimpleNamespace:
     return SimpleNamespace(name="hip", linear=linear, rmsnorm=rmsnorm, add_rmsnorm=add_rmsnorm, silu_mul=silu_mul,
                            qk_norm_rope_kv_write=qk_norm_rope_kv_write,
                            paged_attention_decode=paged_attention_decode,
-                           paged_attention_prefill=paged_attention_prefill, sample_step=sample_step,
+                           paged_attention_prefill=paged_attention_prefill,
+                           paged_attention_decode_exp=paged_attention_decode_exp, sample_step=sample_step,
                            library=lib)

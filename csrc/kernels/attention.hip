@@ -25,6 +25,8 @@
 // (flash-decoding).  Prefill: one workgroup per (64-query tile, query
 // head), causal over cached prefix + new tokens, varlen via a tile table.
 
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -52,16 +54,18 @@ struct Chunk {
 };
 
 // Issue every load of one 32-token chunk whose blocks are blk0/blk1.
-template <int HD>
+template <int HD, bool KT = false>
 __device__ __forceinline__ void load_chunk(Chunk<HD>& c, const KVGeom& g, int blk0, int blk1, int kvh, int lane) {
   const int r = lane & 15, h = lane >> 4;
   const size_t b0 = block_base<HD>(g, blk0, kvh), b1 = block_base<HD>(g, blk1, kvh);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int t = 8 * (r >> 2) + 4 * u + (r & 3);
-    const bf16_t* krow = g.k + (t < BS ? b0 : b1) + (t & (BS - 1)) * HD + 8 * h;
+    // KT: K block-head stored [HD/32][BS][32] -> each load instruction reads 256-B runs
+    const bf16_t* krow = g.k + (t < BS ? b0 : b1) + (KT ? (t & (BS - 1)) * 32 : (t & (BS - 1)) * HD) + 8 * h;
 #pragma unroll
-    for (int kk = 0; kk < HD / 32; ++kk) c.k[u][kk] = *reinterpret_cast<const bf16x8*>(krow + kk * 32);
+    for (int kk = 0; kk < HD / 32; ++kk)
+      c.k[u][kk] = *reinterpret_cast<const bf16x8*>(krow + kk * (KT ? BS * 32 : 32));
   }
   const bf16_t* vb = g.v + (h < 2 ? b0 : b1) + 8 * (h & 1);
 #pragma unroll
@@ -154,84 +158,121 @@ struct Causal {
 };
 
 // ------------------------------------------------------------------ decode
-// One workgroup per (sequence, kv head, split); a split is `split_tokens`
-// (multiple of 128) tokens, chosen per launch so that B * n_kv * splits keeps
-// every CU busy (large B => 1-2 splits => little partial-sum traffic).  The 4
-// waves take the split's 32-token chunks round-robin; each wave keeps ONE chunk
-// in registers (~64 VGPRs) so 3-4 waves per SIMD stay resident and hide the HBM
-// latency.  Block ids of a wave's chunks are fetched once (lane i holds chunk
-// i's two block ids) and broadcast with readlane, so no table load sits between
-// K/V loads on the in-order vmcnt counter.
-template <int HD>
+// Work item = (sequence b, 128-token split, kv head): the 4 waves of a
+// workgroup take the item's four 32-token chunks (one each, loaded with 16
+// back-to-back 16-B loads), and the G = n_q / n_kv query heads of the kv head
+// share every K/V byte (GQA packing).  Items are enumerated from the LIVE
+// context lengths -- a prefix sum over ceil(ctx_b / 128) computed by every
+// workgroup into LDS -- and a fixed grid strides over them.  A grid sized from
+// the block-table width instead (graph-safe, but ctx << max_model_len) spent
+// most of its workgroups reading seq_lens only to exit: 78 % of the launch at
+// B = 160, ctx 1700, max_model_len 8192.
+constexpr int DEC_SPLIT = DEC_WAVES * CHUNK;  // 128 tokens per item
+constexpr int DEC_MAX_B = 1024;
+
+template <int HD, bool KT = false>
 __global__ __launch_bounds__(256) void decode_attn_kernel(
     const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
-    const int* __restrict__ seq_lens, int n_q, float scale_log2, float* __restrict__ part_o,
-    float* __restrict__ part_ml, int max_splits, int split_tokens) {
-  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
-  const int ctx = seq_lens[b];
-  const int start = split * split_tokens;
-  if (start >= ctx) return;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r = lane & 15, h = lane >> 4;
-  const int G = n_q / g.n_kv;
-  const int* table = block_tables + static_cast<size_t>(b) * max_blocks;
-
-  bf16x8 bq[HD / 32];
-  load_q<HD>(bq, q + (static_cast<size_t>(b) * n_q + kvh * G + (r < G ? r : 0)) * HD, r < G, lane);
-
-  float m = -INFINITY, l = 0.f;
-  f32x4 o[HD / 16];
-#pragma unroll
-  for (int dt = 0; dt < HD / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int end = min(ctx, start + split_tokens);
-  const int nchunk = (end - start + CHUNK - 1) / CHUNK;     // chunks of this split
-  const int mine = (nchunk - w + DEC_WAVES - 1) / DEC_WAVES;  // chunks of this wave (<= 64)
-  const int last_blk = (ctx - 1) / BS;
-  int e0 = 0, e1 = 0;
-  if (lane < mine) {
-    const int t0 = start + (w + lane * DEC_WAVES) * CHUNK;
-    e0 = table[t0 / BS];
-    e1 = table[min(t0 / BS + 1, last_blk)];
-  }
-  for (int i = 0; i < mine; ++i) {
-    const int t0 = start + (w + i * DEC_WAVES) * CHUNK;
-    Chunk<HD> c;
-    load_chunk<HD>(c, g, __builtin_amdgcn_readlane(e0, i), __builtin_amdgcn_readlane(e1, i), kvh, lane);
-    compute_chunk<HD>(c, bq, t0, end, AllVisible{}, scale_log2, m, l, o, lane);
-  }
-
-  // combine the 4 waves through LDS
+    const int* __restrict__ seq_lens, int B, int n_q, float scale_log2, float* __restrict__ part_o,
+    float* __restrict__ part_ml, int max_splits) {
+  __shared__ int s_pre[DEC_MAX_B + 1];
+  __shared__ int s_wsum[DEC_WAVES];
   __shared__ float s_ml[DEC_WAVES][2][16];
   __shared__ float s_o[DEC_WAVES][HD][16 + 1];
-  if (h == 0) {
-    s_ml[w][0][r] = m;
-    s_ml[w][1][r] = l;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 15, h = lane >> 4;
+  const int G = n_q / g.n_kv;
+
+  // ---- item enumeration: s_pre[b] = sum_{b' < b} ceil(ctx_b' / 128)
+  {
+    const int per = (B + 255) / 256;  // <= 4
+    int cnt[4], sum = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = tid * per + j;
+      cnt[j] = (j < per && i < B) ? (seq_lens[i] + DEC_SPLIT - 1) / DEC_SPLIT : 0;
+      sum += cnt[j];
+    }
+    int incl = sum;  // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, WAVE);
+      if (lane >= o) incl += v;
+    }
+    if (lane == 63) s_wsum[w] = incl;
+    __syncthreads();
+    int base = incl - sum;
+    for (int ww = 0; ww < w; ++ww) base += s_wsum[ww];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = tid * per + j;
+      if (j < per && i < B) s_pre[i] = base;
+      base += cnt[j];
+    }
+    if (tid == 255) s_pre[B] = base;
+    __syncthreads();
   }
-#pragma unroll
-  for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) s_o[w][dt * 16 + 4 * h + i][r] = o[dt][i];
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < G * HD; idx += blockDim.x) {
-    const int qi = idx / HD, d = idx % HD;
-    float mm = -INFINITY;
-#pragma unroll
-    for (int ww = 0; ww < DEC_WAVES; ++ww) mm = fmaxf(mm, s_ml[ww][0][qi]);
-    float ll = 0.f, oo = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < DEC_WAVES; ++ww) {
-      const float mw = s_ml[ww][0][qi];
-      const float f = mw == -INFINITY ? 0.f : exp2f(mw - mm);
-      ll += s_ml[ww][1][qi] * f;
-      oo += s_o[ww][d][qi] * f;
+  const int n_items = s_pre[B] * g.n_kv;
+
+  for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
+    const int pos = item / g.n_kv, kvh = item - pos * g.n_kv;
+    int lo = 0, hi = B - 1;  // last b with s_pre[b] <= pos (binary search, wave-uniform)
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_pre[mid] <= pos) lo = mid; else hi = mid - 1;
     }
-    const size_t pidx = (static_cast<size_t>(b) * n_q + kvh * G + qi) * max_splits + split;
-    part_o[pidx * HD + d] = oo;
-    if (d == 0) {
-      part_ml[pidx * 2] = mm;
-      part_ml[pidx * 2 + 1] = ll;
+    const int b = lo, split = pos - s_pre[b];
+    const int ctx = seq_lens[b];
+    const int start = split * DEC_SPLIT;
+    const int* table = block_tables + static_cast<size_t>(b) * max_blocks;
+
+    bf16x8 bq[HD / 32];
+    load_q<HD>(bq, q + (static_cast<size_t>(b) * n_q + kvh * G + (r < G ? r : 0)) * HD, r < G, lane);
+    float m = -INFINITY, l = 0.f;
+    f32x4 o[HD / 16];
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int t0 = start + w * CHUNK;
+    if (t0 < ctx) {  // wave-uniform
+      const int last_blk = (ctx - 1) / BS;
+      const int e0 = table[t0 / BS], e1 = table[min(t0 / BS + 1, last_blk)];
+      Chunk<HD> c;
+      load_chunk<HD, KT>(c, g, e0, e1, kvh, lane);
+      compute_chunk<HD>(c, bq, t0, ctx, AllVisible{}, scale_log2, m, l, o, lane);
     }
+
+    // combine the 4 waves through LDS
+    if (h == 0) {
+      s_ml[w][0][r] = m;
+      s_ml[w][1][r] = l;
+    }
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s_o[w][dt * 16 + 4 * h + i][r] = o[dt][i];
+    __syncthreads();
+    for (int idx = tid; idx < G * HD; idx += blockDim.x) {
+      const int qi = idx / HD, d = idx % HD;
+      float mm = -INFINITY;
+#pragma unroll
+      for (int ww = 0; ww < DEC_WAVES; ++ww) mm = fmaxf(mm, s_ml[ww][0][qi]);
+      float ll = 0.f, oo = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < DEC_WAVES; ++ww) {
+        const float mw = s_ml[ww][0][qi];
+        const float f = mw == -INFINITY ? 0.f : exp2f(mw - mm);
+        ll += s_ml[ww][1][qi] * f;
+        oo += s_o[ww][d][qi] * f;
+      }
+      const size_t pidx = (static_cast<size_t>(b) * n_q + kvh * G + qi) * max_splits + split;
+      part_o[pidx * HD + d] = oo;
+      if (d == 0) {
+        part_ml[pidx * 2] = mm;
+        part_ml[pidx * 2 + 1] = ll;
+      }
+    }
+    __syncthreads();  // s_o / s_ml are rewritten by the next item
   }
 }
 
@@ -257,15 +298,25 @@ __global__ __launch_bounds__(HD) void decode_combine_kernel(const float* __restr
   out[static_cast<size_t>(bq) * HD + d] = f2bf(ll > 0.f ? oo / ll : 0.f);
 }
 
-template <int HD>
+template <int HD, bool KT = false>
 void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks, const int* seq_lens, int B,
-                   int n_q, float sl, float* ws, int max_splits, int split_tokens, bf16_t* out, hipStream_t stream) {
+                   int n_q, float sl, float* ws, int max_splits, bf16_t* out, hipStream_t stream) {
   float* part_o = ws;
   float* part_ml = ws + static_cast<size_t>(B) * n_q * max_splits * HD;
-  hipLaunchKernelGGL(decode_attn_kernel<HD>, dim3(max_splits, g.n_kv, B), dim3(256), 0, stream, q, g, tables,
-                     max_blocks, seq_lens, n_q, sl, part_o, part_ml, max_splits, split_tokens);
+  // fixed (graph-safe) grid striding over the live items: one full wave of resident workgroups
+  static int resident = 0;
+  if (resident == 0) {
+    int per_cu = 0, cus = 0, dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_attn_kernel<HD, KT>, 256, 0);
+    resident = std::max(1, per_cu) * std::max(1, cus);
+  }
+  const int grid = static_cast<int>(std::min<long>(static_cast<long>(B) * g.n_kv * max_splits, resident));
+  hipLaunchKernelGGL((decode_attn_kernel<HD, KT>), dim3(grid), dim3(256), 0, stream, q, g, tables, max_blocks,
+                     seq_lens, B, n_q, sl, part_o, part_ml, max_splits);
   hipLaunchKernelGGL(decode_combine_kernel<HD>, dim3(B * n_q), dim3(HD), 0, stream, part_o, part_ml, seq_lens,
-                     n_q, max_splits, split_tokens, out);
+                     n_q, max_splits, DEC_SPLIT, out);
 }
 
 // ----------------------------------------------------------------- prefill
@@ -339,33 +390,48 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
 
 // Split size for a decode batch.  Measured on MI355X (tools/bench_ops.py,
 // Qwen3-14B geometry, ctx 1700, B 40-192): one 32-token chunk per wave (128
-// tokens per workgroup) reaches 3.0-3.2 TB/s; looping waves over several
-// chunks (256-2048-token splits) stays at 2.0-2.6 TB/s even with every chunk's
-// 16 loads issued together -- short-lived workgroups keep more loads in
-// flight per CU than long ones at 3 waves/SIMD.
-BCG_API int bcg_decode_split_tokens(int B, int n_kv, int max_tokens) { return 128; }
+// tokens per work item) beats looping waves over several chunks (256-2048-token
+// splits: 2.0-2.6 TB/s against 3.0-3.2) -- more independent loads in flight
+// per CU at 3 waves/SIMD.
+BCG_API int bcg_decode_split_tokens(int B, int n_kv, int max_tokens) { return DEC_SPLIT; }
 
 BCG_API int bcg_paged_attention_decode(const void* q, const void* k_cache, const void* v_cache, int layer,
                                        int num_blocks, int n_kv, const int* block_tables, int max_blocks,
                                        const int* seq_lens, int B, int n_q, int hd, int block_size,
                                        float scale, float* workspace, int max_splits, int split_tokens,
                                        void* out, hipStream_t stream) {
-  if (block_size != BS || n_q % n_kv || n_q / n_kv > 16 || B <= 0) return -2;
-  if (split_tokens % 128 || split_tokens > DEC_WAVES * 64 * CHUNK || max_splits * split_tokens < max_blocks * BS)
-    return -3;
+  if (block_size != BS || n_q % n_kv || n_q / n_kv > 16 || B <= 0 || B > DEC_MAX_B) return -2;
+  if (split_tokens != DEC_SPLIT || max_splits * split_tokens < max_blocks * BS) return -3;
   KVGeom g{static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), layer, num_blocks, n_kv};
   const bf16_t* qb = static_cast<const bf16_t*>(q);
   bf16_t* ob = static_cast<bf16_t*>(out);
   const float sl = scale * LOG2E;
   if (hd == 128) {
-    launch_decode<128>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace, max_splits, split_tokens,
-                       ob, stream);
+    launch_decode<128>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace, max_splits, ob, stream);
   } else if (hd == 64) {
-    launch_decode<64>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace, max_splits, split_tokens,
-                      ob, stream);
+    launch_decode<64>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace, max_splits, ob, stream);
   } else {
     return -2;
   }
+  return BCG_CHECK_LAUNCH();
+}
+
+// Timing-only variants for tools/bench_ops.py (results are NOT valid attention
+// for the engine's cache layout): variant 1 = K read as [HD/32][BS][32] tiles.
+BCG_API int bcg_paged_attention_decode_exp(const void* q, const void* k_cache, const void* v_cache, int layer,
+                                           int num_blocks, int n_kv, const int* block_tables, int max_blocks,
+                                           const int* seq_lens, int B, int n_q, int hd, float scale,
+                                           float* workspace, int max_splits, int split_tokens, void* out,
+                                           int variant, hipStream_t stream) {
+  if (hd != 128 || n_q / n_kv > 16 || split_tokens != DEC_SPLIT || B > DEC_MAX_B) return -2;
+  KVGeom g{static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), layer, num_blocks, n_kv};
+  const float sl = scale * LOG2E;
+  if (variant == 1)
+    launch_decode<128, true>(static_cast<const bf16_t*>(q), g, block_tables, max_blocks, seq_lens, B, n_q, sl,
+                             workspace, max_splits, static_cast<bf16_t*>(out), stream);
+  else
+    launch_decode<128, false>(static_cast<const bf16_t*>(q), g, block_tables, max_blocks, seq_lens, B, n_q, sl,
+                              workspace, max_splits, static_cast<bf16_t*>(out), stream);
   return BCG_CHECK_LAUNCH();
 }
 

@@ -76,3 +76,45 @@ def test_llm_guided_json_all_schemas():
     eng = llm.backend
     assert eng.stats["cached_tokens"] > 0 or eng.args.kv_block_size > 32
     assert eng.graphs is not None and eng.graphs.captures >= 1
+
+
+def test_continuous_batching_overlapped_prefill():
+    """Async engine thread + prefill stream: clients arrive while earlier rows decode."""
+    import threading
+    from byzantine_consensus_llm_agents_amd.bcg import prompts as P
+    from byzantine_consensus_llm_agents_amd.bcg.config import ENGINE_CONFIG
+    from byzantine_consensus_llm_agents_amd.engine import GuidedDecodingParams, LLM, SamplingParams
+    ENGINE_CONFIG["budget_aware_json"] = True
+    llm = LLM("bcg/tiny-qwen3", backend="hip", seed=9, max_model_len=4096, kv_cache_gb=2.0,
+              overlap_prefill=True)
+    assert llm.backend.overlap
+    llm.start_continuous_batching()
+    schemas = [P.honest_decision_schema(0, 50), P.vote_schema(P.HONEST_VOTE_OPTIONS)]
+    results, errors = {}, []
+
+    def client(k):
+        try:
+            for rnd in range(3):
+                prompts = [f"<|im_start|>system\nagent_{k}_{j} " + "history line. " * (50 * (j + 1))
+                           + f"<|im_end|>\n<|im_start|>user\nround {rnd}<|im_end|>\n<|im_start|>assistant\n"
+                           for j in range(4)]
+                params = [SamplingParams(temperature=0.5, max_tokens=[120, 20][j % 2],
+                                         guided_decoding=GuidedDecodingParams(json=schemas[j % 2]))
+                          for j in range(4)]
+                outs = llm.generate(prompts, params)
+                for o, p in zip(outs, params):
+                    obj = json.loads(o.outputs[0].text)
+                    assert set(p.guided_decoding.json["required"]) <= set(obj)
+            results[k] = True
+        except BaseException as exc:
+            errors.append(exc)
+
+    threads = [threading.Thread(target=client, args=(k,)) for k in range(12)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    llm.shutdown()
+    ENGINE_CONFIG["budget_aware_json"] = False
+    assert not errors, errors[0]
+    assert len(results) == 12

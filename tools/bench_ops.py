@@ -66,11 +66,13 @@ def main():
             out["gemm"].append(rec)
             print(json.dumps(rec), flush=True)
     # decode attention at the bench geometry
-    NB = 1 + (args.ctx // 16 + 1) * 192
+    b_list = [int(b) for b in os.environ.get("BCG_BENCH_B", "8,40,160,192").split(",")]
+    NB = 1 + (args.ctx // 16 + 1) * max(b_list)  # every row's table must stay inside the cache
     k = torch.randn(1, NB, cfg.num_kv_heads, 16, hd, device="cuda", dtype=torch.bfloat16)
     v = torch.randn(1, NB, cfg.num_kv_heads, hd, 16, device="cuda", dtype=torch.bfloat16)
-    for B in [int(b) for b in os.environ.get("BCG_BENCH_B", "8,40,160,192").split(",")]:
+    for B in b_list:
         nb = (args.ctx + 15) // 16
+        assert B * nb + 1 <= NB
         tables = (torch.arange(B * nb, dtype=torch.int32, device="cuda").view(B, nb) + 1)
         tables = torch.cat([tables, torch.zeros(B, 512 - nb, dtype=torch.int32, device="cuda")], 1).contiguous()
         seq = torch.full((B,), args.ctx, dtype=torch.int32, device="cuda")
@@ -78,6 +80,9 @@ def main():
         t = timeit(lambda: hip.paged_attention_decode(q, k, v, 0, tables, seq, hd ** -0.5))
         gb = B * args.ctx * cfg.num_kv_heads * hd * 2 * 2 / 1e9
         rec = {"B": B, "ctx": args.ctx, "us": round(t, 1), "TBps": round(gb / t * 1e3, 2)}
+        for variant in [int(x) for x in os.environ.get("BCG_ATTN_VARIANTS", "").split(",") if x]:
+            tv = timeit(lambda: hip.paged_attention_decode_exp(q, k, v, 0, tables, seq, hd ** -0.5, variant))
+            rec[f"v{variant}_TBps"] = round(gb / tv * 1e3, 2)
         out["attention"].append(rec)
         print(json.dumps(rec), flush=True)
     # sampler
