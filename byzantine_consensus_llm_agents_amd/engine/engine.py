@@ -508,24 +508,24 @@ class InferenceEngine:
         return t.pin_memory().to(self.device, non_blocking=True)
 
     def _plan_prefill(self, wave: List[_Seq], table_cpu: torch.Tensor) -> List[tuple]:
-        """Split the uncached prompt tokens into packed chunks; upload every chunk's metadata first."""
+        """Pack the uncached prompt tokens into chunks of exactly `prefill_chunk_tokens`
+        (a prompt may straddle chunks; only the last chunk is shorter), so the
+        prefill GEMMs run at one M that the shipped TunableOp table covers.
+        Every chunk's metadata is uploaded before any forward is launched."""
         budget = self.args.prefill_chunk_tokens
-        segments = []  # (row, start, end) of uncached prompt tokens
+        plans, chunk, used = [], [], 0
         for r, s in enumerate(wave):
             pos, n = s.cached, len(s.prompt_ids)
             while pos < n:
-                end = min(n, pos + budget)
-                segments.append((r, pos, end))
-                pos = end
-        plans, chunk, used = [], [], 0
-        for seg in segments + [None]:
-            if seg is not None and used + (seg[2] - seg[1]) <= budget:
-                chunk.append(seg)
-                used += seg[2] - seg[1]
-                continue
-            if chunk:
-                plans.append(self._plan_chunk(wave, chunk, table_cpu))
-            chunk, used = ([seg], seg[2] - seg[1]) if seg is not None else ([], 0)
+                take = min(n - pos, budget - used)
+                chunk.append((r, pos, pos + take))
+                used += take
+                pos += take
+                if used == budget:
+                    plans.append(self._plan_chunk(wave, chunk, table_cpu))
+                    chunk, used = [], 0
+        if chunk:
+            plans.append(self._plan_chunk(wave, chunk, table_cpu))
         return plans
 
     def _plan_chunk(self, wave, chunk, table_cpu):

@@ -75,3 +75,25 @@ def test_continuous_batching_threads(llm):
     assert len(results) == 5
     for outs, params in results.values():
         _check(outs, params)
+
+
+def test_chunked_prefill_matches_single_chunk(llm):
+    """Prompts straddling prefill chunks (odd chunk size) give the same greedy outputs."""
+    from byzantine_consensus_llm_agents_amd.engine import GuidedDecodingParams, SamplingParams
+    eng = llm.backend
+    prompts = [f"<|im_start|>system\nagent {i} " + "long history entry. " * (6 + 5 * i)
+               + "<|im_end|>\n<|im_start|>assistant\n" for i in range(4)]
+    params = [SamplingParams(temperature=0.0, max_tokens=40,
+                             guided_decoding=GuidedDecodingParams(json=SCHEMAS[i % 4])) for i in range(4)]
+    saved = (eng.args.prefill_chunk_tokens, eng.args.prefix_caching)
+    try:
+        eng.args.prefix_caching = False
+        eng.args.prefill_chunk_tokens = 1 << 14
+        ref = [o.outputs[0].text for o in llm.generate(prompts, params)]
+        eng.args.prefill_chunk_tokens = 37
+        chunks0 = eng.stats["prefill_chunks"]
+        got = [o.outputs[0].text for o in llm.generate(prompts, params)]
+        assert eng.stats["prefill_chunks"] - chunks0 > 4
+    finally:
+        eng.args.prefill_chunk_tokens, eng.args.prefix_caching = saved
+    assert got == ref

@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--top", type=int, default=12)
+    ap.add_argument("--window", type=float, default=0.0, help="also print GPU idle %% per window of this many s")
     a = ap.parse_args()
     opener = gzip.open if a.trace.endswith(".gz") else open
     ev = []
@@ -61,6 +62,27 @@ def main():
                           "top": [(n, round(t / 1e6, 1)) for n, t in per_q_names[q].most_common(a.top)]}
                       for q, v in sorted(per_q.items())}}
     print(json.dumps(out, indent=1))
+    if a.window > 0:
+        w = int(a.window * 1e9)
+        nwin = (t1 - t0) // w + 1
+        busy_w = [0] * nwin
+        # merge intervals, then spread the busy time over windows
+        cur_s, cur_e = ev[0][0], ev[0][1]
+        merged = []
+        for s, e, _, _ in ev[1:]:
+            if s <= cur_e:
+                cur_e = max(cur_e, e)
+            else:
+                merged.append((cur_s, cur_e))
+                cur_s, cur_e = s, e
+        merged.append((cur_s, cur_e))
+        for s, e in merged:
+            while s < e:
+                k = (s - t0) // w
+                edge = t0 + (k + 1) * w
+                busy_w[k] += min(e, edge) - s
+                s = min(e, edge)
+        print("idle % per window:", " ".join(f"{100 - 100 * b / w:.0f}" for b in busy_w))
 
 
 if __name__ == "__main__":

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--max-m", type=int, default=512)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--extra-m", default="", help="comma list of extra M (e.g. prefill chunk 16384; no lm_head)")
+    ap.add_argument("--base", default=None, help="existing TunableOp CSV to extend (results are kept)")
     args = ap.parse_args()
     cfg = get_model_config(args.model)
     name = ALIASES.get(args.model, args.model).split("/")[-1].lower()
@@ -43,10 +45,15 @@ def main():
     torch.cuda.tunable.tuning_enable(True)
     torch.cuda.tunable.set_max_tuning_duration(40)
     torch.cuda.tunable.set_filename(out)
+    if args.base and os.path.exists(args.base):
+        torch.cuda.tunable.read_file(args.base)
     ws = {k: torch.randn(n, kk, device="cuda", dtype=torch.bfloat16) for k, (n, kk) in shapes.items()}
     t0 = time.time()
-    for M in [b for b in BUCKETS if b <= args.max_m]:
+    extra = [int(m) for m in args.extra_m.split(",") if m]
+    for M in [b for b in BUCKETS if b <= args.max_m] + extra:
         for k, w in ws.items():
+            if M > 4096 and k == "lm_head":
+                continue  # prefill computes logits for the last token of each sequence only
             x = torch.randn(M, w.shape[1], device="cuda", dtype=torch.bfloat16)
             torch.nn.functional.linear(x, w)
         torch.cuda.synchronize()
