@@ -137,6 +137,12 @@ class InferenceEngine:
             else:
                 self.model.init_random(seed=args.seed or 0)
         self.seed = (args.seed if args.seed is not None else int.from_bytes(os.urandom(4), "little")) & 0x7FFFFFFF
+        if self.tp.size > 1:  # TP ranks sample identically: share rank 0's seed
+            t = torch.tensor([self.seed], dtype=torch.int64,
+                             device=self.device if self.device.type == "cuda" else "cpu")
+            torch.distributed.broadcast(t, src=torch.distributed.get_global_rank(self.tp.group, 0),
+                                        group=self.tp.group)
+            self.seed = int(t.item())
         self._req_counter = 0
 
         self.fsm = FSMRegistry(self.tokenizer.all_token_bytes(), cfg.vocab_size, self.device,

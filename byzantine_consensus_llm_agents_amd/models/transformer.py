@@ -165,6 +165,37 @@ class DecoderModel:
         self.final_norm = get("model.norm.weight")
         self._finish()
 
+    def hf_state_dict(self) -> Dict[str, torch.Tensor]:
+        """HF-named full state dict (TP=1 only): inverse of `load_hf_state_dict`."""
+        if self.tp.size != 1:
+            raise ValueError("hf_state_dict exports unsharded weights (tp=1)")
+        c, hd = self.cfg, self.hd
+        nq, nkv = self.n_q * hd, self.n_kv * hd
+        sd = {}
+        for i, L in enumerate(self.layers):
+            p = f"model.layers.{i}."
+            q, k, v = L["qkv"].split([nq, nkv, nkv])
+            sd[p + "self_attn.q_proj.weight"], sd[p + "self_attn.k_proj.weight"] = q, k
+            sd[p + "self_attn.v_proj.weight"] = v
+            sd[p + "self_attn.o_proj.weight"] = L["o"]
+            g, u = L["gate_up"].split([self.inter, self.inter])
+            sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"] = g, u
+            sd[p + "mlp.down_proj.weight"] = L["down"]
+            sd[p + "input_layernorm.weight"] = L["ln1"]
+            sd[p + "post_attention_layernorm.weight"] = L["ln2"]
+            if c.qkv_bias:
+                qb, kb, vb = L["qkv_bias"].split([nq, nkv, nkv])
+                sd[p + "self_attn.q_proj.bias"], sd[p + "self_attn.k_proj.bias"] = qb, kb
+                sd[p + "self_attn.v_proj.bias"] = vb
+            if c.qk_norm:
+                sd[p + "self_attn.q_norm.weight"] = L["q_norm"]
+                sd[p + "self_attn.k_norm.weight"] = L["k_norm"]
+        sd["model.embed_tokens.weight"] = self.embed
+        if not c.tie_embeddings:
+            sd["lm_head.weight"] = self.lm_head
+        sd["model.norm.weight"] = self.final_norm
+        return {k: t.contiguous() for k, t in sd.items()}
+
     def _finish(self):
         from ..ops.reference import rope_cache
         c = self.cfg

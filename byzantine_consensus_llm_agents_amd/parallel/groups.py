@@ -1,0 +1,124 @@
+"""Process-group layout: one process per GPU, TP groups of consecutive ranks, DP across groups.
+
+The reference delegates tensor parallelism to vLLM's multiprocessing executor
+(``bcg/vllm_agent.py:126-142``: ``tensor_parallel_size`` +
+``distributed_executor_backend='mp'``) and has no data parallelism inside a
+run (``bcg/main.py:1073`` ``run_simulation`` is the external sweep hook).
+Here both are explicit:
+
+* ranks ``[g*tp, (g+1)*tp)`` form TP group ``g`` (RCCL all-reduce over xGMI:
+  consecutive ranks of one node are direct xGMI peers on an MI355X OAM board);
+* the ``world // tp`` groups are data-parallel replicas that run independent
+  simulation seeds and only meet for the final result reduction.
+
+``torch.distributed`` with backend ``"nccl"`` is RCCL on ROCm; CPU tests use
+``"gloo"`` with the same code path.
+"""
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..models.transformer import TPGroup
+
+
+@dataclass(frozen=True)
+class Layout:
+    world: int
+    rank: int
+    local_rank: int
+    tp: int
+
+    @property
+    def dp(self) -> int:
+        return self.world // self.tp
+
+    @property
+    def tp_rank(self) -> int:
+        return self.rank % self.tp
+
+    @property
+    def dp_rank(self) -> int:
+        return self.rank // self.tp
+
+    @property
+    def is_group_leader(self) -> bool:
+        return self.tp_rank == 0
+
+
+_TP_GROUPS = {}
+_DP_GROUPS = {}
+
+
+def env_layout(tp: int = 1) -> Layout:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world % tp:
+        raise ValueError(f"world size {world} not divisible by tensor_parallel_size {tp}")
+    return Layout(world, rank, local, tp)
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) -> Layout:
+    """Initialise the default process group from torchrun's env (idempotent).
+
+    Backend: RCCL (``"nccl"``) when a GPU is visible, gloo otherwise.  The
+    rendezvous address defaults to 127.0.0.1 (single node; the container
+    hostname may not resolve).
+    """
+    lay = env_layout()
+    if lay.world == 1 or dist.is_initialized():
+        return lay
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29511")
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    if backend is None:
+        backend = "nccl" if torch.cuda.device_count() > 0 else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(lay.local_rank)
+    dist.init_process_group(backend, rank=lay.rank, world_size=lay.world,
+                            timeout=datetime.timedelta(seconds=timeout_s))
+    return lay
+
+
+def tensor_parallel_group(tp: int) -> TPGroup:
+    """TPGroup of this rank (every rank must call this with the same `tp`)."""
+    if tp <= 1:
+        return TPGroup()
+    if not dist.is_initialized():
+        init_distributed()
+    lay = env_layout(tp)
+    if dist.get_world_size() != lay.world:
+        lay = Layout(dist.get_world_size(), dist.get_rank(), lay.local_rank, tp)
+    if tp not in _TP_GROUPS:
+        mine = None
+        for g in range(lay.world // tp):  # new_group is collective over ALL ranks
+            ranks = list(range(g * tp, (g + 1) * tp))
+            pg = dist.new_group(ranks)
+            if lay.rank in ranks:
+                mine = pg
+        _TP_GROUPS[tp] = mine
+    return TPGroup(_TP_GROUPS[tp], lay.tp_rank, tp)
+
+
+def data_parallel_group(tp: int):
+    """Group of the TP-rank-0 processes (one per replica) for result reduction; None if world == tp."""
+    if not dist.is_initialized():
+        return None
+    world = dist.get_world_size()
+    if world == tp:
+        return None
+    if tp not in _DP_GROUPS:
+        _DP_GROUPS[tp] = dist.new_group(list(range(0, world, tp)))
+    return _DP_GROUPS[tp]
+
+
+def destroy():
+    _TP_GROUPS.clear()
+    _DP_GROUPS.clear()
+    if dist.is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,147 @@
+"""Model numerics on CPU: HF transformers parity, checkpoint IO, tensor parallelism (gloo, 2 ranks)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from byzantine_consensus_llm_agents_amd.models.batch import alloc_kv, prefill_batch
+from byzantine_consensus_llm_agents_amd.models.config import get_model_config
+from byzantine_consensus_llm_agents_amd.models.loader import load_safetensors_dir, save_hf_checkpoint
+from byzantine_consensus_llm_agents_amd.models.transformer import DecoderModel, TPGroup
+from byzantine_consensus_llm_agents_amd.ops import get_ops
+
+SEQS = [[5, 17, 99, 1000, 7, 7, 42] * 5, [3, 1, 4, 1, 5, 9, 2, 6, 5, 3, 5], list(range(100, 160))]
+
+
+def _model(name, tp=None, seed=1):
+    cfg = get_model_config(name)
+    m = DecoderModel(cfg, get_ops("torch"), "cpu", torch.float32, tp)
+    m.init_random(seed=seed, std=0.05)
+    return m
+
+
+def _forward(m, seqs=SEQS):
+    tokens, meta, nblk = prefill_batch(seqs)
+    k, v = alloc_kv(m, nblk)
+    return m.forward(tokens, meta, k, v)
+
+
+@pytest.mark.parametrize("name,hf_cls", [("bcg/tiny-qwen3", "Qwen3ForCausalLM"),
+                                         ("bcg/tiny-qwen2", "Qwen2ForCausalLM"),
+                                         ("bcg/tiny-mistral", "MistralForCausalLM")])
+def test_matches_hf_transformers(name, hf_cls, tmp_path):
+    """Last-token logits of the paged engine model == HF transformers' eager forward (parity pinned)."""
+    import transformers
+    from byzantine_consensus_llm_agents_amd.models.loader import hf_config_dict
+    m = _model(name)
+    ours = _forward(m)
+    cfg_d = hf_config_dict(m.cfg)
+    cfg_d.pop("torch_dtype")
+    arch_cfg = {"Qwen3ForCausalLM": transformers.Qwen3Config, "Qwen2ForCausalLM": transformers.Qwen2Config,
+                "MistralForCausalLM": transformers.MistralConfig}[hf_cls]
+    hf_cfg = arch_cfg(**{k: v for k, v in cfg_d.items() if k != "model_type"})
+    hf_cfg._attn_implementation = "eager"
+    hf = getattr(transformers, hf_cls)(hf_cfg).float().eval()
+    missing, unexpected = hf.load_state_dict(m.hf_state_dict(), strict=False)
+    tied = {"lm_head.weight"} if m.cfg.tie_embeddings else set()
+    assert not unexpected and all("rotary" in k or k in tied for k in missing), (missing, unexpected)
+    if tied:
+        assert hf.lm_head.weight.data_ptr() == hf.model.embed_tokens.weight.data_ptr()
+    for r, s in enumerate(SEQS):
+        with torch.no_grad():
+            ref = hf(torch.tensor([s])).logits[0, -1]
+        torch.testing.assert_close(ours[r], ref, atol=2e-4, rtol=2e-4)
+
+
+def test_checkpoint_roundtrip_sharded(tmp_path):
+    m = _model("bcg/tiny-qwen2")  # QKV bias + tied embeddings
+    save_hf_checkpoint(m.hf_state_dict(), m.cfg, str(tmp_path), max_shard_bytes=4 << 20)
+    assert os.path.exists(tmp_path / "model.safetensors.index.json")
+    cfg = get_model_config("x", str(tmp_path))
+    assert cfg.qkv_bias and cfg.tie_embeddings and cfg.num_layers == m.cfg.num_layers
+    m2 = DecoderModel(cfg, get_ops("torch"), "cpu", torch.float32)
+    m2.load_hf_state_dict(load_safetensors_dir(str(tmp_path)))
+    torch.testing.assert_close(_forward(m2), _forward(m), atol=0, rtol=0)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _tp_worker(rank, world, port, ckpt, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from byzantine_consensus_llm_agents_amd.parallel import groups
+    groups.init_distributed("gloo")
+    tp = groups.tensor_parallel_group(world)
+    cfg = get_model_config("x", ckpt)
+    m = DecoderModel(cfg, get_ops("torch"), "cpu", torch.float32, tp)
+    m.load_hf_state_dict(load_safetensors_dir(ckpt))
+    logits = _forward(m)
+    if rank == 0:
+        torch.save(logits, out)
+    groups.destroy()
+
+
+def test_tensor_parallel_2_ranks_matches_tp1(tmp_path):
+    m = _model("bcg/tiny-qwen3")
+    ckpt = str(tmp_path / "ckpt")
+    save_hf_checkpoint(m.hf_state_dict(), m.cfg, ckpt)
+    out = str(tmp_path / "logits.pt")
+    mp.start_processes(_tp_worker, args=(2, _free_port(), ckpt, out), nprocs=2, join=True, start_method="spawn")
+    got = torch.load(out, weights_only=True)
+    torch.testing.assert_close(got, _forward(m), atol=1e-4, rtol=1e-4)
+
+
+def test_tp_group_identity_without_distributed():
+    g = TPGroup()
+    x = torch.ones(3, 4)
+    assert g.all_reduce_(x) is x and g.all_gather_last(x) is x
+
+
+def _engine_tp_worker(rank, world, port, ckpt, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import json
+    from byzantine_consensus_llm_agents_amd.parallel import groups
+    groups.init_distributed("gloo")
+    texts = _engine_texts(ckpt, tp=world, seed=None if rank else 11)  # rank 0's seed must win
+    with open(f"{out}.{rank}", "w") as fh:
+        json.dump(texts, fh)
+    groups.destroy()
+
+
+def _engine_texts(ckpt, tp, seed):
+    from byzantine_consensus_llm_agents_amd.bcg import prompts as P
+    from byzantine_consensus_llm_agents_amd.engine import GuidedDecodingParams, LLM, SamplingParams
+    llm = LLM("bcg/tiny-qwen3", backend="torch", weights=ckpt, tensor_parallel_size=tp, seed=seed,
+              max_model_len=512, kv_cache_gb=0.05, max_batch_seqs=8, dtype=torch.float32,
+              budget_aware_json=True)
+    schemas = [P.honest_decision_schema(0, 50), P.vote_schema(P.BYZANTINE_VOTE_OPTIONS)]
+    prompts = [f"<|im_start|>user\nagent_{i} proposes {i * 7}<|im_end|>\n<|im_start|>assistant\n"
+               for i in range(6)]
+    params = [SamplingParams(temperature=[0.0, 0.5][i % 2], max_tokens=48,
+                             guided_decoding=GuidedDecodingParams(json=schemas[i % 2])) for i in range(6)]
+    texts = [o.outputs[0].text for o in llm.generate(prompts, params)]
+    llm.shutdown()
+    return texts
+
+
+def test_engine_tensor_parallel_lockstep(tmp_path):
+    """TP=2 engines (gloo) stay in lock-step and reproduce the TP=1 engine's outputs (same seed)."""
+    import json
+    m = _model("bcg/tiny-qwen3")
+    ckpt = str(tmp_path / "ckpt")
+    save_hf_checkpoint(m.hf_state_dict(), m.cfg, ckpt)
+    out = str(tmp_path / "texts")
+    mp.start_processes(_engine_tp_worker, args=(2, _free_port(), ckpt, out), nprocs=2, join=True,
+                       start_method="spawn")
+    r0, r1 = (json.load(open(f"{out}.{r}")) for r in range(2))
+    assert r0 == r1
+    assert r0 == _engine_texts(ckpt, tp=1, seed=11)
+    for t in r0:
+        json.loads(t)
