@@ -1,0 +1,126 @@
+"""Guided-decoding compiler (byte DFA -> token FSM) and the native runtime (token FSM, block manager)."""
+import json
+import random
+
+import numpy as np
+import pytest
+
+
+from byzantine_consensus_llm_agents_amd.bcg import prompts as P
+from byzantine_consensus_llm_agents_amd.engine.guided.compiler import compile_schema, compile_token_fsm_py
+from byzantine_consensus_llm_agents_amd.engine.guided.json_schema import integer_node, schema_to_dfa
+from byzantine_consensus_llm_agents_amd.engine.guided.regex_dfa import compile_dfa
+from byzantine_consensus_llm_agents_amd.runtime import BlockManager, compile_token_fsm
+
+SCHEMAS = {
+    "honest_decide": P.honest_decision_schema(0, 50),
+    "byz_decide": P.byzantine_decision_schema(0, 50),
+    "honest_vote": P.vote_schema(P.HONEST_VOTE_OPTIONS),
+    "byz_vote": P.vote_schema(P.BYZANTINE_VOTE_OPTIONS),
+}
+
+
+@pytest.mark.parametrize("lo,hi", [(0, 50), (0, 9), (7, 123), (-20, 15), (100, 100)])
+def test_integer_range_dfa_exact(lo, hi):
+    dfa = compile_dfa(integer_node(lo, hi))
+    for v in range(lo - 30, hi + 31):
+        assert dfa.matches(str(v).encode()) == (lo <= v <= hi), v
+    for bad in (b"", b"-", b"01" if lo <= 1 <= hi else b"00", b"+5", b"1.0"):
+        assert not dfa.matches(bad)
+
+
+def test_schema_dfa_accepts_valid_and_rejects_invalid():
+    dfa = schema_to_dfa(SCHEMAS["honest_decide"], max_ws=4)
+    ok = [{"internal_strategy": "x", "value": 7, "public_reasoning": "y"},
+          {"internal_strategy": "q\\\"uote é", "value": 50, "public_reasoning": ""}]
+    for obj in ok:
+        assert dfa.matches(json.dumps(obj).encode()), obj
+        assert dfa.matches(json.dumps(obj, indent=1).encode()), obj
+    bad = [{"internal_strategy": "x", "value": 51, "public_reasoning": "y"},
+           {"internal_strategy": "x", "value": 3},
+           {"internal_strategy": "x", "value": 3, "public_reasoning": "y", "extra": 1}]
+    for obj in bad:
+        assert not dfa.matches(json.dumps(obj).encode()), obj
+    byz = schema_to_dfa(SCHEMAS["byz_decide"], max_ws=4)
+    assert byz.matches(b'{"internal_strategy": "s", "value": "abstain"}')
+    assert byz.matches(b'{"internal_strategy": "s", "value": 12, "public_reasoning": "r"}')
+    vote = schema_to_dfa(SCHEMAS["byz_vote"], max_ws=4)
+    assert vote.matches(b'{"decision": "abstain"}') and not vote.matches(b'{"decision": "maybe"}')
+
+
+def test_bounded_whitespace():
+    dfa = schema_to_dfa(SCHEMAS["honest_vote"], max_ws=2)
+    assert dfa.matches(b'{  "decision":  "stop"}')
+    assert not dfa.matches(b'{   "decision": "stop"}')
+
+
+def _toy_vocab(seed=0, n=600):
+    rng = random.Random(seed)
+    alphabet = b'{}":, abcdeinoprstuvlgy0123456789-_\n\\'
+    toks = [bytes([b]) for b in range(256)]
+    while len(toks) < n:
+        toks.append(bytes(rng.choice(alphabet) for _ in range(rng.randint(2, 6))))
+    return toks + [b""]  # an empty (special) token is never allowed
+
+
+@pytest.mark.parametrize("name", sorted(SCHEMAS))
+def test_native_token_fsm_matches_python_oracle(name):
+    vocab = _toy_vocab()
+    dfa = schema_to_dfa(SCHEMAS[name], max_ws=4)
+    nxt_c, dist_c = compile_token_fsm(dfa.trans, dfa.accept.astype(np.uint8), vocab, len(vocab) + 3)
+    nxt_p, dist_p = compile_token_fsm_py(dfa.trans, dfa.accept, vocab, len(vocab) + 3)
+    np.testing.assert_array_equal(np.asarray(nxt_c), nxt_p)
+    np.testing.assert_array_equal(np.asarray(dist_c), dist_p)
+
+
+def test_token_fsm_walk_generates_only_valid_json():
+    """Random walks restricted to allowed tokens that respect dist[] always end in schema-valid JSON."""
+    vocab = _toy_vocab(seed=3)
+    for name, schema in SCHEMAS.items():
+        fsm = compile_schema(schema, vocab, len(vocab), max_ws=4)
+        dfa = schema_to_dfa(schema, max_ws=4)
+        rng = random.Random(hash(name) & 0xFFFF)
+        for _ in range(20):
+            s, out, budget = 0, b"", 80
+            while True:
+                allowed = [t for t in range(len(vocab)) if fsm.next[s, t] >= 0
+                           and fsm.dist[fsm.next[s, t]] <= budget - 1]
+                if fsm.dist[s] == 0 and (not allowed or rng.random() < 0.3):
+                    break
+                assert allowed, (name, out)
+                t = rng.choice(allowed)
+                out += vocab[t]
+                s = int(fsm.next[s, t])
+                budget -= 1
+            assert dfa.matches(out), out
+            obj = json.loads(out)
+            assert set(schema["required"]) <= set(obj) <= set(schema["properties"])
+
+
+def test_block_manager_prefix_cache_and_eviction():
+    bm = BlockManager(8, 4)  # 8 blocks of 4 tokens
+    prompt = list(range(10))  # 2 full blocks + 2 tokens
+    a = bm.allocate(prompt, 3, True)
+    assert a.ok and a.num_cached_tokens == 0 and len(a.blocks) == 4  # ceil(13 / 4)
+    bm.commit_prompt(list(a.blocks), prompt)
+    b = bm.allocate(prompt[:8] + [99, 98], 2, True)
+    assert b.ok and b.num_cached_tokens == 8 and list(b.blocks[:2]) == list(a.blocks[:2])
+    bm.free(list(a.blocks))
+    bm.free(list(b.blocks))
+    assert bm.num_free_blocks == 8
+    # cached blocks are evicted (LRU) when the pool runs dry
+    big = bm.allocate(list(range(100, 132)), 0, True)
+    assert big.ok and len(big.blocks) == 8 and bm.evictions >= 2
+    assert not bm.allocate([1, 2, 3], 1, True).ok
+    bm.free(list(big.blocks))
+    assert bm.num_free_blocks == 8
+
+
+def test_block_manager_partial_prompt_never_fully_cached():
+    """At least one prompt token is always recomputed (its logits start decoding)."""
+    bm = BlockManager(16, 4)
+    prompt = list(range(8))  # exactly 2 blocks
+    a = bm.allocate(prompt, 1, True)
+    bm.commit_prompt(list(a.blocks), prompt)
+    b = bm.allocate(prompt, 1, True)
+    assert b.ok and b.num_cached_tokens < len(prompt)
