@@ -396,16 +396,17 @@ class InferenceEngine:
             logits.record_stream(torch.cuda.current_stream())
         st, dev = self.state, self.device
         seqs = [r.seq for r in reqs]
-        rows_d = torch.tensor([r.row for r in reqs], dtype=torch.long).to(dev)
-        st["block_tables"].index_copy_(0, rows_d, fl["table"].to(dev))
+        rows_d = self._h2d(torch.tensor([r.row for r in reqs], dtype=torch.long))
+        st["block_tables"].index_copy_(0, rows_d, self._h2d(fl["table"]))
         vals = {"seq_lens": [len(s.prompt_ids) for s in seqs], "fsm_base": [s.fsm_base for s in seqs],
                 "fsm_state": [0] * len(seqs), "gen_count": [0] * len(seqs),
                 "max_new": [s.max_new for s in seqs], "row_keys": [self._next_key() for _ in seqs],
                 "done": [0] * len(seqs), "next_tokens": [0] * len(seqs)}
-        for key, v in vals.items():
-            st[key].index_copy_(0, rows_d, torch.tensor(v, dtype=torch.int32).to(dev))
-        st["temperature"].index_copy_(0, rows_d, torch.tensor([s.temperature for s in seqs],
-                                                               dtype=torch.float32).to(dev))
+        packed = self._h2d(torch.tensor(list(vals.values()), dtype=torch.int32))  # one upload
+        for i, key in enumerate(vals):
+            st[key].index_copy_(0, rows_d, packed[i])
+        st["temperature"].index_copy_(0, rows_d, self._h2d(torch.tensor([s.temperature for s in seqs],
+                                                                         dtype=torch.float32)))
         for s in seqs:  # prompt blocks are now resident: make them reusable
             self.blocks.commit_prompt(s.blocks, s.prompt_ids)
             self.stats["prompt_tokens"] += len(s.prompt_ids)
@@ -438,13 +439,12 @@ class InferenceEngine:
         if not rows:
             return
         n = rows[-1] + 1
-        done = self.state["done"][:n].tolist()
+        done, counts = torch.stack([self.state["done"][:n], self.state["gen_count"][:n]]).tolist()
         finished = [i for i in rows if done[i]]
         if not finished:
             return
         with self.timer.phase("detokenize"):
-            counts = self.state["gen_count"][:n].tolist()
-            idx = torch.tensor(finished, dtype=torch.long, device=self.device)
+            idx = self._h2d(torch.tensor(finished, dtype=torch.long))
             outs = self.state["out_tokens"].index_select(0, idx).tolist()
             for i, toks in zip(finished, outs):
                 req = self.slots[i]
@@ -463,7 +463,7 @@ class InferenceEngine:
         """Inactive rows: done, context 1 on the scratch block (harmless in the graph)."""
         if not rows:
             return
-        idx = torch.tensor(rows, dtype=torch.long, device=self.device)
+        idx = self._h2d(torch.tensor(rows, dtype=torch.long))
         st = self.state
         st["done"].index_fill_(0, idx, 1)
         st["seq_lens"].index_fill_(0, idx, 1)
@@ -486,8 +486,8 @@ class InferenceEngine:
         movers = [i for i in reversed(live) if i >= len(occupied)][:len(free)]
         if not movers:
             return
-        src = torch.tensor(movers, dtype=torch.long, device=self.device)
-        dst = torch.tensor(free[:len(movers)], dtype=torch.long, device=self.device)
+        src = self._h2d(torch.tensor(movers, dtype=torch.long))
+        dst = self._h2d(torch.tensor(free[:len(movers)], dtype=torch.long))
         for key, t in self.state.items():
             t.index_copy_(0, dst, t.index_select(0, src))
         for a, b in zip(movers, free):
