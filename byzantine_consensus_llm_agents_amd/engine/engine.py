@@ -129,7 +129,7 @@ class InferenceEngine:
         self.tokenizer = load_tokenizer(args.model, model_dir)
         if self.tokenizer.vocab_size > cfg.vocab_size:
             raise ValueError("tokenizer larger than the model vocabulary")
-        self.model = DecoderModel(cfg, self.ops, self.device, args.dtype, self.tp)
+        self.model = DecoderModel(cfg, self.ops, self.device, args.dtype, self.tp, quant=args.quantization)
         with self.timer.phase("load_weights"):
             if model_dir:
                 from ..models.loader import load_safetensors_dir

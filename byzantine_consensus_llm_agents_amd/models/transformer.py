@@ -59,8 +59,13 @@ class TPGroup:
 
 
 class DecoderModel:
+    PROJECTIONS = ("qkv", "o", "gate_up", "down")
+
     def __init__(self, cfg: ModelConfig, ops, device, dtype=torch.bfloat16,
-                 tp: Optional[TPGroup] = None):
+                 tp: Optional[TPGroup] = None, quant: Optional[str] = None):
+        if quant not in (None, "fp8"):
+            raise ValueError(f"unsupported quantization {quant!r} (None or 'fp8')")
+        self.quant = quant
         self.cfg = cfg
         self.ops = ops
         self.device = torch.device(device)
@@ -167,8 +172,8 @@ class DecoderModel:
 
     def hf_state_dict(self) -> Dict[str, torch.Tensor]:
         """HF-named full state dict (TP=1 only): inverse of `load_hf_state_dict`."""
-        if self.tp.size != 1:
-            raise ValueError("hf_state_dict exports unsharded weights (tp=1)")
+        if self.tp.size != 1 or self.quant:
+            raise ValueError("hf_state_dict exports unsharded, unquantised weights (tp=1, bf16)")
         c, hd = self.cfg, self.hd
         nq, nkv = self.n_q * hd, self.n_kv * hd
         sd = {}
@@ -197,8 +202,15 @@ class DecoderModel:
         return {k: t.contiguous() for k, t in sd.items()}
 
     def _finish(self):
-        from ..ops.reference import rope_cache
+        from ..ops.reference import quantize_weight_fp8, rope_cache
         c = self.cfg
+        if self.quant == "fp8":
+            # per-output-channel e4m3fn weights (+ fp32 scales) replace the bf16 projections;
+            # embedding, norms and the LM head stay bf16 (as vLLM's fp8 path)
+            for L in self.layers:
+                for name in self.PROJECTIONS:
+                    if L[name].dtype != torch.float8_e4m3fn:
+                        L[name], L[name + "_s"] = quantize_weight_fp8(L[name])
         self.cos_sin = rope_cache(min(c.max_position, 65536), self.hd, c.rope_theta, self.device)
 
     def weight_bytes(self) -> int:
@@ -215,9 +227,14 @@ class DecoderModel:
         ops, c = self.ops, self.cfg
         x = F.embedding(tokens.long(), self.embed)
         residual = None
+        fp8 = self.quant == "fp8"
         for li, L in enumerate(self.layers):
-            h, residual = ops.add_rmsnorm(x, residual, L["ln1"], c.rms_eps)
-            qkv = ops.linear(h, L["qkv"], L.get("qkv_bias"))
+            if fp8:  # norm + row-wise fp8 quant fused; hipBLASLt fp8 GEMM
+                hq, hs, residual = ops.add_rmsnorm_fp8(x, residual, L["ln1"], c.rms_eps)
+                qkv = ops.linear_fp8(hq, hs, L["qkv"], L["qkv_s"], L.get("qkv_bias"))
+            else:
+                h, residual = ops.add_rmsnorm(x, residual, L["ln1"], c.rms_eps)
+                qkv = ops.linear(h, L["qkv"], L.get("qkv_bias"))
             q = ops.qk_norm_rope_kv_write(qkv, meta.positions, meta.slots, self.n_q, self.n_kv, self.hd,
                                           L.get("q_norm"), L.get("k_norm"), c.rms_eps, self.cos_sin,
                                           k_cache, v_cache, li)
@@ -228,10 +245,18 @@ class DecoderModel:
                 attn = ops.paged_attention_prefill(q, k_cache, v_cache, li, meta.block_tables,
                                                    meta.q_start, meta.seq_lens, self.scale, meta.max_q_len,
                                                    meta.tiles)
-            x = self.tp.all_reduce_(ops.linear(attn, L["o"]))
-            h, residual = ops.add_rmsnorm(x, residual, L["ln2"], c.rms_eps)
-            gu = ops.linear(h, L["gate_up"])
-            x = self.tp.all_reduce_(ops.linear(ops.silu_mul(gu), L["down"]))
+            if fp8:
+                aq, as_ = ops.quant_fp8(attn)
+                x = self.tp.all_reduce_(ops.linear_fp8(aq, as_, L["o"], L["o_s"]))
+                hq, hs, residual = ops.add_rmsnorm_fp8(x, residual, L["ln2"], c.rms_eps)
+                gu = ops.linear_fp8(hq, hs, L["gate_up"], L["gate_up_s"])
+                mq, ms = ops.silu_mul_fp8(gu)
+                x = self.tp.all_reduce_(ops.linear_fp8(mq, ms, L["down"], L["down_s"]))
+            else:
+                x = self.tp.all_reduce_(ops.linear(attn, L["o"]))
+                h, residual = ops.add_rmsnorm(x, residual, L["ln2"], c.rms_eps)
+                gu = ops.linear(h, L["gate_up"])
+                x = self.tp.all_reduce_(ops.linear(ops.silu_mul(gu), L["down"]))
         if meta.logits_idx is not None:
             x = x.index_select(0, meta.logits_idx)
             residual = residual.index_select(0, meta.logits_idx)

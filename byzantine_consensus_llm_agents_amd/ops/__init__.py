@@ -31,6 +31,10 @@ def _torch_ops() -> SimpleNamespace:
         paged_attention_prefill=prefill,
         silu_mul=_ref.silu_mul,
         sample_step=_ref.sample_step,
+        quant_fp8=_ref.quant_fp8,
+        add_rmsnorm_fp8=_ref.add_rmsnorm_fp8,
+        silu_mul_fp8=_ref.silu_mul_fp8,
+        linear_fp8=_ref.linear_fp8,
     )
 
 

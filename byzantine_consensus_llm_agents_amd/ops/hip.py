@@ -47,6 +47,10 @@ def load_library(path: str = None) -> ctypes.CDLL:
                                            c_void_p, c_int, c_void_p],
         "bcg_gemm_skinny": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                             c_void_p],
+        "bcg_quant_fp8": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+        "bcg_add_rmsnorm_fp8": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_int,
+                                c_void_p],
+        "bcg_silu_mul_fp8": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
         "bcg_guided_sample": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                               c_uint32, c_int, c_int, c_int, c_int, c_void_p],
@@ -206,7 +210,49 @@ def hip_ops() -> SimpleNamespace:
             out_tokens.shape[1], _p(next_tokens), seed & 0xFFFFFFFF, int(bool(budget_aware)), n_text_tokens,
             eos_id, eos_id2, _stream()), "guided_sample")
 
-    return SimpleNamespace(name="hip", linear=linear, rmsnorm=rmsnorm, add_rmsnorm=add_rmsnorm, silu_mul=silu_mul,
+    f8 = torch.float8_e4m3fn
+
+    def quant_fp8(x):
+        _req(x.dtype == torch.bfloat16 and x.is_contiguous() and x.dim() == 2 and x.shape[1] % 8 == 0,
+             "quant_fp8: bf16 [T,K], K % 8 == 0")
+        T, K = x.shape
+        q = torch.empty(T, K, dtype=f8, device=x.device)
+        s = torch.empty(T, dtype=torch.float32, device=x.device)
+        _check(lib.bcg_quant_fp8(_p(x), _p(q), _p(s), T, K, _stream()), "quant_fp8")
+        return q, s
+
+    def add_rmsnorm_fp8(x, residual, w, eps):
+        _req(x.dtype == torch.bfloat16 and x.is_contiguous() and x.dim() == 2, "add_rmsnorm_fp8: x bf16 [T,H]")
+        T, H = x.shape
+        _req(w.shape == (H,) and w.dtype == torch.bfloat16, "add_rmsnorm_fp8: weight [H] bf16")
+        has_res = residual is not None
+        if not has_res:
+            residual = torch.empty_like(x)
+        else:
+            _req(residual.shape == x.shape and residual.is_contiguous(), "add_rmsnorm_fp8: residual shape")
+        q = torch.empty(T, H, dtype=f8, device=x.device)
+        s = torch.empty(T, dtype=torch.float32, device=x.device)
+        _check(lib.bcg_add_rmsnorm_fp8(_p(x), _p(residual), _p(w), _p(q), _p(s), T, H, eps, int(has_res),
+                                       _stream()), "add_rmsnorm_fp8")
+        return q, s, residual
+
+    def silu_mul_fp8(gu):
+        _req(gu.dtype == torch.bfloat16 and gu.is_contiguous() and gu.dim() == 2 and gu.shape[1] % 16 == 0,
+             "silu_mul_fp8: bf16 [T,2I]")
+        T, I2 = gu.shape
+        q = torch.empty(T, I2 // 2, dtype=f8, device=gu.device)
+        s = torch.empty(T, dtype=torch.float32, device=gu.device)
+        _check(lib.bcg_silu_mul_fp8(_p(gu), _p(q), _p(s), T, I2 // 2, _stream()), "silu_mul_fp8")
+        return q, s
+
+    def linear_fp8(xq, xs, wq, ws, bias=None, out_dtype=torch.bfloat16):
+        """hipBLASLt fp8 GEMM (torch._scaled_mm) with row-wise activation and weight scales."""
+        _req(xq.dtype == f8 and wq.dtype == f8 and xq.shape[1] == wq.shape[1], "linear_fp8 operands")
+        return torch._scaled_mm(xq, wq.t(), scale_a=xs.view(-1, 1), scale_b=ws.view(1, -1), bias=bias,
+                                out_dtype=out_dtype)
+
+    return SimpleNamespace(name="hip", linear=linear, quant_fp8=quant_fp8, add_rmsnorm_fp8=add_rmsnorm_fp8,
+                           silu_mul_fp8=silu_mul_fp8, linear_fp8=linear_fp8, rmsnorm=rmsnorm, add_rmsnorm=add_rmsnorm, silu_mul=silu_mul,
                            qk_norm_rope_kv_write=qk_norm_rope_kv_write,
                            paged_attention_decode=paged_attention_decode,
                            paged_attention_prefill=paged_attention_prefill,

@@ -203,3 +203,40 @@ def sample_step(logits: torch.Tensor, fsm_next: torch.Tensor, fsm_dist: torch.Te
             finished = finished or tok in (eos_id, eos_id2)
         if finished:
             done[b] = 1
+
+
+# ------------------------------------------------------------------ fp8 (OCP e4m3fn)
+FP8_MAX = 448.0
+FP8 = torch.float8_e4m3fn
+
+
+def quant_fp8(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Row-wise dynamic quantisation: scale = max|x_row| / 448, q = x / scale (fp8 e4m3fn)."""
+    xf = x.float()
+    scale = xf.abs().amax(dim=-1).clamp(min=1e-12) / FP8_MAX
+    q = (xf / scale[:, None]).clamp(-FP8_MAX, FP8_MAX).to(FP8)
+    return q, scale
+
+
+def add_rmsnorm_fp8(x, residual, w, eps):
+    """add_rmsnorm (bf16-rounded output, as the bf16 path) then row-wise fp8 quantisation."""
+    y, residual = add_rmsnorm(x, residual, w, eps)
+    q, s = quant_fp8(y)
+    return q, s, residual
+
+
+def silu_mul_fp8(gu):
+    return quant_fp8(silu_mul(gu))
+
+
+def quantize_weight_fp8(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-output-channel weight quantisation: w [N, K] -> (fp8 [N, K], scale fp32 [N])."""
+    return quant_fp8(w)
+
+
+def linear_fp8(xq, xs, wq, ws, bias=None, out_dtype=torch.bfloat16):
+    """y = (xq * xs[:, None]) @ (wq * ws[:, None])^T (+ bias), fp32 accumulate."""
+    y = (xq.float() * xs[:, None]) @ (wq.float() * ws[:, None]).t()
+    if bias is not None:
+        y = y + bias.float()
+    return y.to(out_dtype)

@@ -7,23 +7,24 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _models(name):
+def _models(name, quant=None):
     from byzantine_consensus_llm_agents_amd.models.config import get_model_config
     from byzantine_consensus_llm_agents_amd.models.transformer import DecoderModel
     from byzantine_consensus_llm_agents_amd.ops import get_ops
     cfg = get_model_config(name)
     out = []
     for backend in ("hip", "torch"):
-        m = DecoderModel(cfg, get_ops(backend), "cuda", torch.bfloat16)
+        m = DecoderModel(cfg, get_ops(backend), "cuda", torch.bfloat16, quant=quant)
         m.init_random(seed=3, std=0.05)
         out.append(m)
     return cfg, out
 
 
-@pytest.mark.parametrize("name", ["bcg/tiny-qwen3", "bcg/tiny-qwen2", "bcg/tiny-mistral"])
-def test_forward_hip_matches_torch(name):
+@pytest.mark.parametrize("name,quant", [("bcg/tiny-qwen3", None), ("bcg/tiny-qwen2", None),
+                                        ("bcg/tiny-mistral", None), ("bcg/tiny-mistral", "fp8")])
+def test_forward_hip_matches_torch(name, quant):
     from byzantine_consensus_llm_agents_amd.models.transformer import AttnMeta
-    cfg, (mh, mt) = _models(name)
+    cfg, (mh, mt) = _models(name, quant)
     torch.manual_seed(0)
     lens = [5, 33, 70]
     T = sum(lens)

@@ -175,3 +175,48 @@ def test_gemm_skinny(hip, M, N, K, bias):
     ref = torch.nn.functional.linear(x.float(), w.float(), None if b is None else b.float())
     out = hip.linear(x, w, b)
     _close(out, ref, atol=2e-2, rtol=2e-2)
+
+
+def _fp8_close(q, s, q_ref, s_ref):
+    """Same row scales; quantised values within one e4m3 step of the reference.
+
+    v_cvt_pk_fp8_f32 and torch's float->e4m3fn cast disagree on ~2 % of
+    elements by one step (rounding of near-tie values), so exact equality is
+    only required for the large majority."""
+    torch.testing.assert_close(s, s_ref, atol=0, rtol=1e-6)
+    a, b = q.float() * s[:, None], q_ref.float() * s_ref[:, None]
+    step = s_ref[:, None] * 448 / 8  # coarsest e4m3 spacing at the row max
+    assert ((a - b).abs() <= step).all()
+    assert (q.float() == q_ref.float()).float().mean() > 0.95
+
+
+@pytest.mark.parametrize("T,K", [(1, 5120), (37, 6144), (300, 896)])
+def test_quant_fp8(hip, T, K):
+    x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16) * 3
+    _fp8_close(*hip.quant_fp8(x), *R.quant_fp8(x))
+
+
+@pytest.mark.parametrize("H,has_res", [(6144, True), (5120, False)])
+def test_add_rmsnorm_fp8(hip, H, has_res):
+    x = torch.randn(23, H, device="cuda", dtype=torch.bfloat16)
+    w = (torch.rand(H, device="cuda") + 0.5).to(torch.bfloat16)
+    res = torch.randn(23, H, device="cuda", dtype=torch.bfloat16) if has_res else None
+    q_ref, s_ref, r_ref = R.add_rmsnorm_fp8(x, None if res is None else res.clone(), w, 1e-5)
+    q, s, r = hip.add_rmsnorm_fp8(x, None if res is None else res.clone(), w, 1e-5)
+    _close(r, r_ref, atol=0, rtol=0)
+    _fp8_close(q, s, q_ref, s_ref)
+
+
+def test_silu_mul_fp8(hip):
+    gu = torch.randn(11, 2 * 16384, device="cuda", dtype=torch.bfloat16)
+    _fp8_close(*hip.silu_mul_fp8(gu), *R.silu_mul_fp8(gu))
+
+
+def test_linear_fp8(hip):
+    x = torch.randn(64, 6144, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(8192, 6144, device="cuda", dtype=torch.bfloat16) * 0.02
+    xq, xs = hip.quant_fp8(x)
+    wq, ws = R.quantize_weight_fp8(w)
+    y = hip.linear_fp8(xq, xs, wq, ws)
+    y_ref = R.linear_fp8(xq, xs, wq, ws)
+    _close(y, y_ref, atol=2e-2, rtol=2e-2)

@@ -145,3 +145,28 @@ def test_engine_tensor_parallel_lockstep(tmp_path):
     assert r0 == _engine_texts(ckpt, tp=1, seed=11)
     for t in r0:
         json.loads(t)
+
+
+@pytest.mark.parametrize("name", ["bcg/tiny-mistral", "bcg/tiny-qwen3"])
+def test_fp8_model_tracks_bf16(name):
+    """fp8 (e4m3fn, row-wise scales) projections stay close to the unquantised model."""
+    ref = _model(name)
+    cfg = ref.cfg
+    m8 = DecoderModel(cfg, get_ops("torch"), "cpu", torch.bfloat16, quant="fp8")
+    m8.load_hf_state_dict(ref.hf_state_dict())
+    assert m8.layers[0]["qkv"].dtype == torch.float8_e4m3fn and m8.layers[0]["qkv_s"].shape == (
+        m8.layers[0]["qkv"].shape[0],)
+    a, b = _forward(ref).float(), _forward(m8).float()
+    cos = torch.nn.functional.cosine_similarity(a, b, dim=-1)
+    assert cos.min() > 0.99, cos
+    assert (a.argmax(-1) == b.argmax(-1)).float().mean() >= 2 / 3
+
+
+def test_quant_fp8_reference_roundtrip():
+    from byzantine_consensus_llm_agents_amd.ops import reference as R
+    x = torch.randn(7, 64) * torch.logspace(-3, 3, 7)[:, None]
+    q, s = R.quant_fp8(x)
+    assert q.dtype == torch.float8_e4m3fn and s.shape == (7,)
+    assert (q.float().abs().amax(-1) == 448).all()
+    back = q.float() * s[:, None]
+    assert ((back - x).abs() <= x.abs().amax(-1, keepdim=True) / 16).all()  # e4m3: 3 mantissa bits
