@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--max-rounds", type=int, default=50)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--backend", default="hip")
+    ap.add_argument("--quantization", default=None, choices=["fp8"])
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--verbose", action="store_true")
@@ -156,6 +157,7 @@ def main():
     C.METRICS_CONFIG["save_results"] = False
     C.VLLM_CONFIG["model_name"] = model
     C.VLLM_CONFIG["tensor_parallel_size"] = args.tp
+    C.VLLM_CONFIG["quantization"] = args.quantization
     C.ENGINE_CONFIG.update(backend=args.backend, budget_aware_json=True, seed=args.seed + rank // args.tp,
                            use_hip_graphs=not args.no_graphs, prefix_caching=not args.no_prefix_cache)
     C.BCG_CONFIG["value_range"] = (0, 50)
@@ -164,7 +166,8 @@ def main():
     t0 = time.perf_counter()
     llm = LLM(model, max_model_len=C.VLLM_CONFIG["max_model_len"],
               gpu_memory_utilization=C.VLLM_CONFIG["gpu_memory_utilization"],
-              tensor_parallel_size=args.tp, backend=args.backend, seed=args.seed + rank // args.tp)
+              tensor_parallel_size=args.tp, backend=args.backend, seed=args.seed + rank // args.tp,
+              quantization=args.quantization)
     # share the engine with every agent (same model name + config => no reload)
     EngineAgent._shared_llm = llm
     EngineAgent._shared_model_name = model
@@ -217,12 +220,13 @@ def main():
     d_eng = {k: eng.get(k, 0) - stats0.get(k, 0) for k in eng}
     if rank == 0:
         line = {
-            "metric": "agent decisions/sec (node), 8h+2b BCG Qwen3-14B; consensus-rate parity",
+            "metric": f"agent decisions/sec (node), {args.honest}h+{args.byzantine}b BCG {model.split('/')[-1]}; "
+                      "consensus-rate parity",
             "value": round(value, 3), "unit": "decisions/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / max(args.steps, 1), 2),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
-            "dtype": "bf16",
+            "dtype": "fp8" if args.quantization == "fp8" else "bf16",
             "data": "synthetic (random-init weights, synthetic BPE tokenizer, budget-aware JSON grammar)",
             "config": {"model": model, "honest": args.honest, "byzantine": args.byzantine,
                        "global_batch": args.sims_per_gpu * (args.honest + args.byzantine) * (world // args.tp),

@@ -39,6 +39,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--seed", type=int, default=None, help="Seed the game and sampler (default: unseeded)")
     p.add_argument("--engine", type=str, default=None, choices=["auto", "hip", "torch", "fake"])
     p.add_argument("--weights", type=str, default=None, help="'random' or a safetensors directory")
+    p.add_argument("--quantization", type=str, default=None, choices=["fp8"],
+                   help="fp8 (e4m3fn) projection GEMMs (the reference only logs this key)")
     p.add_argument("--budget-aware-json", action="store_true",
                    help="Close the JSON before max_tokens instead of truncating")
     return p
@@ -53,6 +55,8 @@ def _apply_engine_flags(args):
         ENGINE_CONFIG["backend"] = args.engine
     if args.weights:
         ENGINE_CONFIG["weights"] = args.weights
+    if args.quantization:
+        VLLM_CONFIG["quantization"] = args.quantization
     if args.seed is not None:
         ENGINE_CONFIG["seed"] = args.seed
     if args.budget_aware_json:

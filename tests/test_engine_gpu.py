@@ -53,7 +53,11 @@ def test_forward_hip_matches_torch(name, quant):
         k = torch.zeros(cfg.num_layers, NB, m.n_kv, bs, m.hd, dtype=torch.bfloat16, device="cuda")
         v = torch.zeros(cfg.num_layers, NB, m.n_kv, m.hd, bs, dtype=torch.bfloat16, device="cuda")
         outs.append(m.forward(tokens, meta, k, v).float())
-    torch.testing.assert_close(outs[0], outs[1], atol=5e-2, rtol=5e-2)
+    if quant is None:
+        torch.testing.assert_close(outs[0], outs[1], atol=5e-2, rtol=5e-2)
+    else:  # one-step fp8 rounding flips (see test_kernels_gpu._fp8_close) compound over layers
+        cos = torch.nn.functional.cosine_similarity(outs[0], outs[1], dim=-1)
+        assert cos.min() > 0.995, cos
 
 
 def test_llm_guided_json_all_schemas():
