@@ -55,6 +55,10 @@ def parse():
     ap.add_argument("--quantization", default=None, choices=["fp8"])
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
+    ap.add_argument("--overlap-prefill", action="store_true",
+                    help="prefill on a second HIP stream, concurrent with decode bursts (TP=1)")
+    ap.add_argument("--no-custom-allreduce", action="store_true",
+                    help="TP collectives through RCCL only (no xGMI one-/two-shot kernels)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -159,7 +163,8 @@ def main():
     C.VLLM_CONFIG["tensor_parallel_size"] = args.tp
     C.VLLM_CONFIG["quantization"] = args.quantization
     C.ENGINE_CONFIG.update(backend=args.backend, budget_aware_json=True, seed=args.seed + rank // args.tp,
-                           use_hip_graphs=not args.no_graphs, prefix_caching=not args.no_prefix_cache)
+                           use_hip_graphs=not args.no_graphs, prefix_caching=not args.no_prefix_cache,
+                           overlap_prefill=args.overlap_prefill, custom_allreduce=not args.no_custom_allreduce)
     C.BCG_CONFIG["value_range"] = (0, 50)
     random.seed(args.seed + rank)
 
@@ -234,7 +239,9 @@ def main():
                        "max_tokens_decide": C.LLM_CONFIG["max_tokens_decide"],
                        "max_tokens_vote": C.LLM_CONFIG["max_tokens_vote"],
                        "parallelism": f"dp{world // args.tp}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
-                       "hip_graphs": not args.no_graphs, "prefix_caching": not args.no_prefix_cache},
+                       "hip_graphs": not args.no_graphs, "prefix_caching": not args.no_prefix_cache,
+                       "overlap_prefill": args.overlap_prefill,
+                       "custom_allreduce": args.tp > 1 and not args.no_custom_allreduce},
             "detail": {"decisions": total_decisions, "elapsed_s": round(elapsed, 3), "init_s": round(init_s, 1),
                        "engine_per_rank": d_eng, "games_finished_rank0": pool.games_finished,
                        "outcomes_rank0": pool.outcomes,

@@ -172,7 +172,8 @@ class InferenceEngine:
         if tp_size <= 1:
             return TPGroup()
         from ..parallel.groups import tensor_parallel_group
-        return tensor_parallel_group(tp_size)
+        return tensor_parallel_group(tp_size, custom_allreduce=(
+            self.backend == "hip" and ENGINE_CONFIG.get("custom_allreduce", True)))
 
     def _alloc_kv_cache(self):
         a, m = self.args, self.model

@@ -40,14 +40,22 @@ class AttnMeta:
 
 
 class TPGroup:
-    """Thin wrapper over a torch.distributed process group (RCCL on ROCm)."""
+    """Thin wrapper over a torch.distributed process group (RCCL on ROCm).
 
-    def __init__(self, group=None, rank: int = 0, size: int = 1):
-        self.group, self.rank, self.size = group, rank, size
+    ``custom`` (optional): an xGMI peer-memory all-reduce
+    (``parallel.custom_allreduce.XGMIAllReduce``) used for every message it
+    accepts -- the decode-sized ones; the rest go through RCCL.
+    """
+
+    def __init__(self, group=None, rank: int = 0, size: int = 1, custom=None):
+        self.group, self.rank, self.size, self.custom = group, rank, size, custom
 
     def all_reduce_(self, x: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
-            torch.distributed.all_reduce(x, group=self.group)
+            if self.custom is not None and self.custom.can(x):
+                self.custom.all_reduce_(x)
+            else:
+                torch.distributed.all_reduce(x, group=self.group)
         return x
 
     def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:

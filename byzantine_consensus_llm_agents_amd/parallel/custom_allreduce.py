@@ -1,0 +1,184 @@
+"""One-shot / two-shot all-reduce over xGMI peer memory (``csrc/kernels/allreduce.hip``).
+
+The reference's TP collectives are NCCL all-reduces inside vLLM
+(``bcg/vllm_agent.py:131,139-142``; SURVEY.md §2.2, §2.3 K-COLL).  On an
+MI355X node every GPU has a direct xGMI link to each of the other seven, so a
+ring (RCCL's default) is per-link bound and pays n-1 latency hops.  Decode
+messages are small -- ``[B, hidden]`` bf16, 10-2000 KiB -- so here each rank
+maps its TP peers' buffers once (``hipIpcGetMemHandle`` exchanged over the
+process group) and a single kernel does the whole collective:
+
+* one-shot (``<= oneshot_max`` bytes): every rank pulls the full message from
+  every peer and reduces locally -- one hop, all links busy at once;
+* two-shot (up to ``cap_bytes``): reduce-scatter + all-gather through the
+  peers' buffers, ``2(n-1)/n`` of the message per rank;
+* larger messages (prefill chunks) and anything that is not contiguous bf16
+  go to RCCL (``torch.distributed.all_reduce``).
+
+Both kernels are graph-capturable (the call epoch lives in device memory) and
+give bitwise-identical results on every rank (fixed summation order).
+``LocalRanks`` builds the same kernels over buffers of ONE process -- the
+in-process multi-stream harness the GPU tests use on a one-GPU box.
+"""
+
+import ctypes
+from typing import List, Optional
+
+import torch
+
+ONESHOT_MAX = 1 << 20          # bytes: one-shot below, two-shot above
+DEFAULT_CAP = 32 << 20         # bytes per message handled by the custom kernels
+THREADS = 512
+
+
+def choose_mode(nbytes: int, world: int, oneshot_max: int = ONESHOT_MAX) -> int:
+    """1 = one-shot, 2 = two-shot (world 8 halves the one-shot limit: 7 full reads per rank)."""
+    limit = oneshot_max if world <= 4 else oneshot_max // 2
+    return 1 if nbytes <= limit else 2
+
+
+def choose_blocks(nbytes: int, world: int, mode: int, max_blocks: int = 128) -> int:
+    """Workgroups per call: ~2 16-B vectors per thread per block, capped at `max_blocks`."""
+    nvec = max(1, nbytes // 16)
+    per_block = THREADS * 2
+    if mode == 2:
+        nvec = (nvec + world - 1) // world
+    return int(max(1, min(max_blocks, (nvec + per_block - 1) // per_block)))
+
+
+def _lib():
+    from ..ops.hip import load_library
+    lib = load_library()
+    P, c_int, c_int64, c_double = ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int64, ctypes.c_double
+    vp = ctypes.c_void_p
+    sig = {"bcg_ar_limits": [ctypes.POINTER(c_int)] * 3,
+           "bcg_ar_alloc": [c_int64, P, P],
+           "bcg_ar_free": [vp],
+           "bcg_ar_ipc_handle_size": [],
+           "bcg_ar_ipc_handle": [vp, vp],
+           "bcg_ar_ipc_open": [vp, P],
+           "bcg_ar_ipc_close": [vp],
+           "bcg_ar_take_error": [vp],
+           "bcg_ar_allreduce": [P, P, c_int, c_int, vp, vp, c_int64, c_int64, c_int, c_int, c_double, vp]}
+    for name, argtypes in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = c_int
+    return lib
+
+
+class _Rank:
+    """One rank's view: pointer tables of every rank's buffers + the launch."""
+
+    def __init__(self, lib, rank: int, world: int, data: List[int], sig: List[int], cap_bytes: int,
+                 oneshot_max: int, timeout_s: float):
+        self.lib, self.rank, self.world = lib, rank, world
+        self.cap_bytes, self.oneshot_max, self.timeout_s = cap_bytes, oneshot_max, timeout_s
+        self._data = (ctypes.c_void_p * world)(*data)
+        self._sig = (ctypes.c_void_p * world)(*sig)
+        mr, mb, sb = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        lib.bcg_ar_limits(ctypes.byref(mr), ctypes.byref(mb), ctypes.byref(sb))
+        if world > mr.value or world & (world - 1):
+            raise ValueError(f"custom all-reduce supports power-of-two groups of <= {mr.value} ranks")
+        self.max_blocks = mb.value
+        self.calls = {1: 0, 2: 0}
+
+    def can(self, x: torch.Tensor) -> bool:
+        n = x.numel()
+        return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and n > 0 and n % 8 == 0
+                and 2 * n <= self.cap_bytes)
+
+    def all_reduce_(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """In-place (or into `out`) sum over the group, on the current (or given) HIP stream."""
+        if not self.can(x):
+            raise ValueError("custom all-reduce: need contiguous bf16 on the GPU, numel % 8 == 0, <= cap")
+        out = x if out is None else out
+        nbytes = 2 * x.numel()
+        mode = choose_mode(nbytes, self.world, self.oneshot_max)
+        blocks = choose_blocks(nbytes, self.world, mode, self.max_blocks)
+        s = (stream or torch.cuda.current_stream()).cuda_stream
+        rc = self.lib.bcg_ar_allreduce(self._data, self._sig, self.rank, self.world,
+                                       ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                       x.numel(), self.cap_bytes, mode, blocks, self.timeout_s,
+                                       ctypes.c_void_p(s))
+        if rc != 0:
+            raise RuntimeError(f"bcg_ar_allreduce launch failed (rc={rc})")
+        self.calls[mode] += 1
+        return out
+
+    def take_error(self) -> bool:
+        """True if a barrier of this rank timed out since the last check (synchronising)."""
+        rc = self.lib.bcg_ar_take_error(self._sig[self.rank])
+        if rc < 0:
+            raise RuntimeError("bcg_ar_take_error failed")
+        return rc == 1
+
+
+def _alloc(lib, cap_bytes: int):
+    d, s = ctypes.c_void_p(), ctypes.c_void_p()
+    if lib.bcg_ar_alloc(cap_bytes, ctypes.byref(d), ctypes.byref(s)) != 0:
+        raise RuntimeError("custom all-reduce: buffer allocation failed")
+    return d.value, s.value
+
+
+class XGMIAllReduce(_Rank):
+    """Custom all-reduce of one TP group (one process per GPU, IPC-mapped peer buffers)."""
+
+    def __init__(self, group, cap_bytes: int = DEFAULT_CAP, oneshot_max: int = ONESHOT_MAX,
+                 timeout_s: float = 30.0):
+        import torch.distributed as dist
+        lib = _lib()
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        d, s = _alloc(lib, cap_bytes)
+        hsz = lib.bcg_ar_ipc_handle_size()
+        hd, hs = ctypes.create_string_buffer(hsz), ctypes.create_string_buffer(hsz)
+        if lib.bcg_ar_ipc_handle(ctypes.c_void_p(d), hd) or lib.bcg_ar_ipc_handle(ctypes.c_void_p(s), hs):
+            raise RuntimeError("custom all-reduce: hipIpcGetMemHandle failed")
+        handles = [None] * world
+        dist.all_gather_object(handles, (hd.raw, hs.raw), group=group)
+        data, sig, self._opened = [], [], []
+        for r, (h_d, h_s) in enumerate(handles):
+            if r == rank:
+                data.append(d)
+                sig.append(s)
+                continue
+            pd, ps = ctypes.c_void_p(), ctypes.c_void_p()
+            if (lib.bcg_ar_ipc_open(ctypes.create_string_buffer(h_d, hsz), ctypes.byref(pd))
+                    or lib.bcg_ar_ipc_open(ctypes.create_string_buffer(h_s, hsz), ctypes.byref(ps))):
+                raise RuntimeError(f"custom all-reduce: hipIpcOpenMemHandle of rank {r} failed")
+            data.append(pd.value)
+            sig.append(ps.value)
+            self._opened += [pd.value, ps.value]
+        self._own = (d, s)
+        super().__init__(lib, rank, world, data, sig, cap_bytes, oneshot_max, timeout_s)
+        dist.barrier(group=group)  # every peer mapped before anyone launches
+
+    def close(self):
+        if self._own is None:
+            return
+        torch.cuda.synchronize()
+        for p in self._opened:
+            self.lib.bcg_ar_ipc_close(ctypes.c_void_p(p))
+        for p in self._own:
+            self.lib.bcg_ar_free(ctypes.c_void_p(p))
+        self._own, self._opened = None, []
+
+
+class LocalRanks:
+    """`world` ranks inside ONE process (buffers on the current GPU): a test harness
+    for the collective kernels on a one-GPU box -- each rank launches on its own stream."""
+
+    def __init__(self, world: int, cap_bytes: int = 4 << 20, oneshot_max: int = ONESHOT_MAX,
+                 timeout_s: float = 5.0):
+        lib = _lib()
+        bufs = [_alloc(lib, cap_bytes) for _ in range(world)]
+        data, sig = [b[0] for b in bufs], [b[1] for b in bufs]
+        self.lib, self._bufs = lib, bufs
+        self.ranks = [_Rank(lib, r, world, data, sig, cap_bytes, oneshot_max, timeout_s) for r in range(world)]
+
+    def close(self):
+        torch.cuda.synchronize()
+        for d, s in self._bufs:
+            self.lib.bcg_ar_free(ctypes.c_void_p(d))
+            self.lib.bcg_ar_free(ctypes.c_void_p(s))
+        self._bufs = []

@@ -52,6 +52,7 @@ class Layout:
 
 _TP_GROUPS = {}
 _DP_GROUPS = {}
+_CUSTOM_AR = {}
 
 
 def env_layout(tp: int = 1) -> Layout:
@@ -85,8 +86,13 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) ->
     return lay
 
 
-def tensor_parallel_group(tp: int) -> TPGroup:
-    """TPGroup of this rank (every rank must call this with the same `tp`)."""
+def tensor_parallel_group(tp: int, custom_allreduce: bool = False) -> TPGroup:
+    """TPGroup of this rank (every rank must call this with the same arguments).
+
+    ``custom_allreduce``: also map the TP peers' buffers for the xGMI one-/two-shot
+    all-reduce kernels (RCCL process groups on GPUs only; set
+    ``BCG_CUSTOM_AR=0`` to force RCCL for every collective).
+    """
     if tp <= 1:
         return TPGroup()
     if not dist.is_initialized():
@@ -102,7 +108,14 @@ def tensor_parallel_group(tp: int) -> TPGroup:
             if lay.rank in ranks:
                 mine = pg
         _TP_GROUPS[tp] = mine
-    return TPGroup(_TP_GROUPS[tp], lay.tp_rank, tp)
+    custom = None
+    if (custom_allreduce and os.environ.get("BCG_CUSTOM_AR", "1") != "0"
+            and dist.get_backend(_TP_GROUPS[tp]) == "nccl"):
+        if tp not in _CUSTOM_AR:
+            from .custom_allreduce import XGMIAllReduce
+            _CUSTOM_AR[tp] = XGMIAllReduce(_TP_GROUPS[tp])
+        custom = _CUSTOM_AR[tp]
+    return TPGroup(_TP_GROUPS[tp], lay.tp_rank, tp, custom=custom)
 
 
 def data_parallel_group(tp: int):
@@ -118,6 +131,9 @@ def data_parallel_group(tp: int):
 
 
 def destroy():
+    for ar in _CUSTOM_AR.values():
+        ar.close()
+    _CUSTOM_AR.clear()
     _TP_GROUPS.clear()
     _DP_GROUPS.clear()
     if dist.is_initialized():
