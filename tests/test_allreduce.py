@@ -69,9 +69,10 @@ def _ref_sum(xs):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,sizes", [(2, [8, 4096, 5120 * 7, 5120 * 100, 5120 * 300 + 8]),
-                                         (4, [5120 * 20, 5120 * 200])])
+@pytest.mark.parametrize("world,sizes", [(2, [8, 4096, 5120 * 7, 5120 * 100, 5120 * 300 + 8])])
 def test_local_ranks_allreduce_bitwise(world, sizes):
+    """In-process: only world 2 -- with GPU_MAX_HW_QUEUES=4 a third or fourth rank stream
+    can share a hardware queue with another rank's spinning kernel (4 ranks: see the IPC test)."""
     lr = CA.LocalRanks(world, cap_bytes=8 << 20, timeout_s=5.0)
     streams = [torch.cuda.Stream() for _ in range(world)]
     try:
@@ -89,9 +90,7 @@ def test_local_ranks_allreduce_bitwise(world, sizes):
                 for r in range(world):
                     assert not lr.ranks[r].take_error(), f"rank {r}: barrier timeout (n={n})"
                     assert torch.equal(bufs[r], ref), f"rank {r} n={n} it={it}"
-        assert lr.ranks[0].calls[1] > 0
-        if world == 2:
-            assert lr.ranks[0].calls[2] > 0  # 5120*300 bf16 = 3 MiB -> two-shot
+        assert lr.ranks[0].calls[1] > 0 and lr.ranks[0].calls[2] > 0  # 5120*300 bf16 = 3 MiB: two-shot
     finally:
         lr.close()
 
@@ -127,9 +126,12 @@ def _ipc_worker(rank, world, port, out):
 
 
 @pytest.mark.gpu
-def test_ipc_two_processes_one_gpu(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_ipc_processes_one_gpu(tmp_path, world):
+    """`world` processes (own HIP queues each) on one GPU, buffers mapped through hipIpc."""
     out = str(tmp_path / "ar")
-    mp.start_processes(_ipc_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
-    for r in range(2):
+    mp.start_processes(_ipc_worker, args=(world, _free_port(), out), nprocs=world, join=True,
+                       start_method="spawn")
+    for r in range(world):
         res = json.load(open(f"{out}.{r}"))
         assert res == {"ok": [True, True, True], "err": False}, (r, res)
