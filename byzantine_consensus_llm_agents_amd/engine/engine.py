@@ -163,6 +163,8 @@ class InferenceEngine:
         self.overlap = bool(args.overlap_prefill and self.device.type == "cuda" and self.tp.size == 1)
         self.prefill_stream = torch.cuda.Stream(self.device) if self.overlap else None
         self._inflight = None
+        self._snap = None        # host copy of (done, gen_count, out_tokens) after the last burst
+        self._snap_buf = None
         if self.backend == "hip" and args.use_hip_graphs:
             from .graphs import DecodeGraphs
             self.graphs = DecodeGraphs(self)
@@ -311,6 +313,7 @@ class InferenceEngine:
 
     def _fail_all(self, exc):
         self._inflight = None
+        self._snap = None
         with self._cv:
             pending = list(self._waiting)
             self._waiting.clear()
@@ -324,13 +327,56 @@ class InferenceEngine:
 
     # ---- one scheduler iteration ----
     def _iterate(self):
+        """reap -> activate prefills -> admit -> decode burst -> snapshot.
+
+        The host never blocks the device between bursts: completion is read
+        from a pinned snapshot taken after the previous burst, and while the
+        device is still running that burst the next one is queued FIRST (rows
+        that finished in it idle one extra burst, harmlessly -- the sampler
+        skips done rows and their blocks are freed only after).  Under TP the
+        early launch is off: it depends on timing, and TP ranks must make
+        identical scheduling decisions.
+        """
+        launched = False
+        snap = self._snap
+        if (snap is not None and self.tp.size == 1 and snap["event"] is not None
+                and not snap["event"].query() and self._live_rows()):
+            self._decode_burst()
+            launched = True
         self._reap()
         if self._inflight is not None and (not self._live_rows() or self._inflight["event"].query()):
             self._finish_prefill()
         if self._inflight is None:
             self._admit()
-        if self._live_rows():
+        if not launched and self._live_rows():
             self._decode_burst()
+        self._take_snapshot()
+
+    def _take_snapshot(self):
+        """Queue a device->pinned-host copy of the completion state of the live rows."""
+        rows = self._live_rows()
+        if not rows:
+            self._snap = None
+            return
+        n = rows[-1] + 1
+        st = self.state
+        if self.device.type != "cuda":
+            self._snap = {"rows": rows, "n": n, "event": None, "done": st["done"][:n].clone(),
+                          "count": st["gen_count"][:n].clone(), "out": st["out_tokens"][:n].clone()}
+            return
+        if self._snap_buf is None:
+            cap = st["done"].shape[0]
+            self._snap_buf = {"done": torch.empty(cap, dtype=torch.int32, pin_memory=True),
+                              "count": torch.empty(cap, dtype=torch.int32, pin_memory=True),
+                              "out": torch.empty(cap, OUT_WIDTH, dtype=torch.int32, pin_memory=True)}
+        h = self._snap_buf
+        h["done"][:n].copy_(st["done"][:n], non_blocking=True)
+        h["count"][:n].copy_(st["gen_count"][:n], non_blocking=True)
+        h["out"][:n].copy_(st["out_tokens"][:n], non_blocking=True)
+        event = torch.cuda.Event()
+        event.record()
+        self._snap = {"rows": rows, "n": n, "event": event, "done": h["done"], "count": h["count"],
+                      "out": h["out"]}
 
     def _active_rows(self) -> List[int]:
         """Occupied rows (decoding, or pending: prefill in flight)."""
@@ -435,18 +481,22 @@ class InferenceEngine:
         return self.args.poll_every
 
     def _reap(self):
-        """Complete finished rows: detokenise, free KV blocks and slots, compact."""
-        rows = self._live_rows()
-        if not rows:
+        """Complete the rows the last snapshot shows finished: detokenise, free KV blocks
+        and slots, park and compact (device ops queued behind any burst in flight)."""
+        snap, self._snap = self._snap, None
+        if snap is None:
             return
-        n = rows[-1] + 1
-        done, counts = torch.stack([self.state["done"][:n], self.state["gen_count"][:n]]).tolist()
-        finished = [i for i in rows if done[i]]
+        if snap["event"] is not None:
+            with self.timer.phase("wait_burst"):
+                snap["event"].synchronize()
+        n = snap["n"]
+        done = snap["done"][:n].tolist()
+        finished = [i for i in snap["rows"] if done[i]]
         if not finished:
             return
+        counts = snap["count"][:n].tolist()
         with self.timer.phase("detokenize"):
-            idx = self._h2d(torch.tensor(finished, dtype=torch.long))
-            outs = self.state["out_tokens"].index_select(0, idx).tolist()
+            outs = snap["out"][finished].tolist()
             for i, toks in zip(finished, outs):
                 req = self.slots[i]
                 toks = toks[:counts[i]]
@@ -604,6 +654,7 @@ class InferenceEngine:
         self._sample(logits, st)
 
     def shutdown(self):
+        self._snap = None
         if self.async_mode:
             with self._cv:
                 self._stop = True
