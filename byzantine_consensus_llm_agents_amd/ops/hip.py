@@ -40,7 +40,7 @@ def load_library(path: str = None) -> ctypes.CDLL:
                                        c_int, c_void_p, c_void_p],
         "bcg_paged_attention_prefill": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
-                                        c_void_p, c_void_p],
+                                        c_void_p, c_int, c_void_p],
         "bcg_decode_split_tokens": [c_int, c_int, c_int],
         "bcg_paged_attention_decode_exp": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                            c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int, c_int,
@@ -154,8 +154,10 @@ def hip_ops() -> SimpleNamespace:
             B, n_q, hd, scale, _p(ws), max_splits, 128, _p(out), variant, _stream()), "decode_exp")
         return out
 
+    prefill_nt = int(os.environ.get("BCG_PREFILL_NT", "4"))  # 16-row query tiles per wave
+
     def paged_attention_prefill(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale,
-                                max_q_len=None, tiles=None):
+                                max_q_len=None, tiles=None, nt=None):
         T, n_q, hd = q.shape
         L, NB, n_kv, BS, _ = k_cache.shape
         _req(tiles is not None and tiles.dtype == torch.int32 and tiles.dim() == 2 and tiles.shape[1] == 3,
@@ -165,8 +167,8 @@ def hip_ops() -> SimpleNamespace:
         out = torch.empty(T, n_q * hd, dtype=q.dtype, device=q.device)
         _check(lib.bcg_paged_attention_prefill(
             _p(q), _p(k_cache), _p(v_cache), layer, NB, n_kv, _p(block_tables), block_tables.shape[1],
-            _p(q_start), _p(seq_lens), _p(tiles), tiles.shape[0], n_q, hd, BS, scale, _p(out), _stream()),
-            "paged_attention_prefill")
+            _p(q_start), _p(seq_lens), _p(tiles), tiles.shape[0], n_q, hd, BS, scale, _p(out),
+            nt or prefill_nt, _stream()), "paged_attention_prefill")
         return out
 
     use_skinny = os.environ.get("BCG_SKINNY_GEMM", "0") == "1"  # hipBLASLt wins (bench_ops r1)

@@ -322,16 +322,26 @@ void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
 // ----------------------------------------------------------------- prefill
 // tiles[i] = {b, q_begin, q_end} (packed row indices); q rows of sequence b occupy
 // [q_start[b], q_start[b+1]) and are its last rows (positions ctx-qlen .. ctx-1).
-template <int HD>
+//
+// A workgroup = 4 waves over one 64-row tile.  Each wave owns NT column tiles
+// of 16 query rows (16*NT rows) of ONE query head and streams the kv head's
+// K/V once for all of them: every 16-B K/V load feeds NT times the MFMAs of
+// the one-tile (NT = 1) form, which was load-bound (L2 -> CU) at 120-200 TF/s.
+// Waves of a block: 4/NT row groups x NT heads; grid = (tiles, ceil(n_q/NT)).
+template <int HD, int NT>
 __global__ __launch_bounds__(256) void prefill_attn_kernel(
     const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
     const int* __restrict__ q_start, const int* __restrict__ seq_lens, const int* __restrict__ tiles,
     int n_q, float scale_log2, bf16_t* __restrict__ out) {
-  const int tile = blockIdx.x, qh = blockIdx.y;
-  const int b = tiles[3 * tile], q_begin = tiles[3 * tile + 1], q_end = tiles[3 * tile + 2];
+  constexpr int RG = 4 / NT;   // row groups per 64-row tile
+  constexpr int ROWS = 16 * NT;
+  const int tile = blockIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int qh = blockIdx.y * NT + w / RG;
+  if (qh >= n_q) return;  // wave-uniform; no block-level barriers in this kernel
+  const int b = tiles[3 * tile], q_begin = tiles[3 * tile + 1], q_end = tiles[3 * tile + 2];
   const int r = lane & 15, h = lane >> 4;
-  const int row0 = q_begin + 16 * w;
+  const int row0 = q_begin + ROWS * (w % RG);
   if (row0 >= q_end) return;
   const int ctx = seq_lens[b];
   const int qs = q_start[b], qlen = q_start[b + 1] - qs;
@@ -339,18 +349,24 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   const int kvh = qh / (n_q / g.n_kv);
   const int* table = block_tables + static_cast<size_t>(b) * max_blocks;
 
-  const int my_row = row0 + r;
-  const bool row_ok = my_row < q_end;
-  const int my_pos = pos0 + (my_row - qs);
-  const int last_row = min(row0 + 15, q_end - 1);
-  const int kv_end = pos0 + (last_row - qs) + 1;  // exclusive bound of keys visible to this wave
-
-  bf16x8 bq[HD / 32];
-  load_q<HD>(bq, q + (static_cast<size_t>(row_ok ? my_row : row0) * n_q + qh) * HD, row_ok, lane);
-  float m = -INFINITY, l = 0.f;
-  f32x4 o[HD / 16];
+  bf16x8 bq[NT][HD / 32];
+  float m[NT], l[NT];
+  f32x4 o[NT][HD / 16];
+  int my_pos[NT], sub_end[NT];  // query position of this lane's column; exclusive key bound per sub-tile
 #pragma unroll
-  for (int dt = 0; dt < HD / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int nt = 0; nt < NT; ++nt) {
+    const int my_row = row0 + 16 * nt + r;
+    const bool ok = my_row < q_end;
+    load_q<HD>(bq[nt], q + (static_cast<size_t>(ok ? my_row : row0) * n_q + qh) * HD, ok, lane);
+    my_pos[nt] = pos0 + (my_row - qs);
+    sub_end[nt] = pos0 + (min(row0 + 16 * nt + 15, q_end - 1) - qs) + 1;
+    m[nt] = -INFINITY;
+    l[nt] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) o[nt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int last_row = min(row0 + ROWS - 1, q_end - 1);
+  const int kv_end = pos0 + (last_row - qs) + 1;  // exclusive bound of keys visible to this wave
 
   // block ids in windows of 64 (one per lane), broadcast with readlane (see decode)
   const int nblk = (kv_end + BS - 1) / BS;
@@ -370,20 +386,51 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   for (int c = 0; c < nchunk; ++c) {
     const int cn = min(c + 1, nchunk - 1);
     load_chunk<HD>(nxt, g, block_at(2 * cn), block_at(min(2 * cn + 1, nblk - 1)), kvh, lane);
-    compute_chunk<HD>(cur, bq, c * CHUNK, kv_end, Causal{my_pos}, scale_log2, m, l, o, lane);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+      if (c * CHUNK < sub_end[nt])  // wave-uniform: skip chunks wholly in this sub-tile's causal future
+        compute_chunk<HD>(cur, bq[nt], c * CHUNK, sub_end[nt], Causal{my_pos[nt]}, scale_log2, m[nt], l[nt],
+                          o[nt], lane);
     cur = nxt;
   }
-  if (!row_ok) return;
-  const float inv = l > 0.f ? 1.f / l : 0.f;
-  bf16_t* orow = out + (static_cast<size_t>(my_row) * n_q + qh) * HD;
-  // O^T rows d = 16dt + 4h + i are this lane's column (query my_row)
 #pragma unroll
-  for (int dt = 0; dt < HD / 16; ++dt) {
-    u16x4 v;
+  for (int nt = 0; nt < NT; ++nt) {
+    const int my_row = row0 + 16 * nt + r;
+    if (my_row >= q_end) continue;
+    const float inv = l[nt] > 0.f ? 1.f / l[nt] : 0.f;
+    bf16_t* orow = out + (static_cast<size_t>(my_row) * n_q + qh) * HD;
+    // O^T rows d = 16dt + 4h + i are this lane's column (query my_row)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = f2bf(o[dt][i] * inv);
-    *reinterpret_cast<u16x4*>(orow + dt * 16 + 4 * h) = v;
+    for (int dt = 0; dt < HD / 16; ++dt) {
+      u16x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = f2bf(o[nt][dt][i] * inv);
+      *reinterpret_cast<u16x4*>(orow + dt * 16 + 4 * h) = v;
+    }
   }
+}
+
+template <int HD>
+int launch_prefill(int nt, int n_tiles, int n_q, const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
+                   const int* q_start, const int* seq_lens, const int* tiles, float sl, bf16_t* out,
+                   hipStream_t stream) {
+  switch (nt) {
+    case 1:
+      hipLaunchKernelGGL((prefill_attn_kernel<HD, 1>), dim3(n_tiles, n_q), dim3(256), 0, stream, q, g, tables,
+                         max_blocks, q_start, seq_lens, tiles, n_q, sl, out);
+      break;
+    case 2:
+      hipLaunchKernelGGL((prefill_attn_kernel<HD, 2>), dim3(n_tiles, (n_q + 1) / 2), dim3(256), 0, stream, q, g,
+                         tables, max_blocks, q_start, seq_lens, tiles, n_q, sl, out);
+      break;
+    case 4:
+      hipLaunchKernelGGL((prefill_attn_kernel<HD, 4>), dim3(n_tiles, (n_q + 3) / 4), dim3(256), 0, stream, q, g,
+                         tables, max_blocks, q_start, seq_lens, tiles, n_q, sl, out);
+      break;
+    default:
+      return -2;
+  }
+  return 0;
 }
 
 }  // namespace
@@ -435,23 +482,25 @@ BCG_API int bcg_paged_attention_decode_exp(const void* q, const void* k_cache, c
   return BCG_CHECK_LAUNCH();
 }
 
+// nt: query tiles of 16 rows per wave (1, 2 or 4) -- see prefill_attn_kernel.
 BCG_API int bcg_paged_attention_prefill(const void* q, const void* k_cache, const void* v_cache, int layer,
                                         int num_blocks, int n_kv, const int* block_tables, int max_blocks,
                                         const int* q_start, const int* seq_lens, const int* tiles, int n_tiles,
-                                        int n_q, int hd, int block_size, float scale, void* out,
+                                        int n_q, int hd, int block_size, float scale, void* out, int nt,
                                         hipStream_t stream) {
   if (block_size != BS || n_q % n_kv || n_tiles <= 0) return -2;
   KVGeom g{static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), layer, num_blocks, n_kv};
   const float sl = scale * LOG2E;
-  dim3 grid(n_tiles, n_q);
-  if (hd == 128) {
-    hipLaunchKernelGGL(prefill_attn_kernel<128>, grid, dim3(256), 0, stream, static_cast<const bf16_t*>(q), g,
-                       block_tables, max_blocks, q_start, seq_lens, tiles, n_q, sl, static_cast<bf16_t*>(out));
-  } else if (hd == 64) {
-    hipLaunchKernelGGL(prefill_attn_kernel<64>, grid, dim3(256), 0, stream, static_cast<const bf16_t*>(q), g,
-                       block_tables, max_blocks, q_start, seq_lens, tiles, n_q, sl, static_cast<bf16_t*>(out));
-  } else {
+  const bf16_t* qb = static_cast<const bf16_t*>(q);
+  bf16_t* ob = static_cast<bf16_t*>(out);
+  int rc;
+  if (hd == 128)
+    rc = launch_prefill<128>(nt, n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens, tiles, sl, ob,
+                             stream);
+  else if (hd == 64)
+    rc = launch_prefill<64>(nt, n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens, tiles, sl, ob,
+                            stream);
+  else
     return -2;
-  }
-  return BCG_CHECK_LAUNCH();
+  return rc ? rc : BCG_CHECK_LAUNCH();
 }

@@ -97,8 +97,9 @@ def _prefill_tiles(q_start, seq_lens):
     return torch.tensor(tiles, dtype=torch.int32, device="cuda")
 
 
-@pytest.mark.parametrize("n_q,n_kv,hd", [(40, 8, 128), (14, 2, 64)])
-def test_paged_attention_prefill(hip, n_q, n_kv, hd):
+@pytest.mark.parametrize("nt", [1, 2, 4])
+@pytest.mark.parametrize("n_q,n_kv,hd", [(40, 8, 128), (14, 2, 64), (48, 8, 128)])
+def test_paged_attention_prefill(hip, n_q, n_kv, hd, nt):
     gen = torch.Generator().manual_seed(3)
     # (cached prefix, new tokens)
     spec = [(0, 1), (0, 37), (16, 50), (32, 64), (0, 300), (160, 129)]
@@ -116,7 +117,7 @@ def test_paged_attention_prefill(hip, n_q, n_kv, hd):
     scale = hd ** -0.5
     ref = R.paged_attention(q, k, v, 0, tables, qs, seq, scale)
     out = hip.paged_attention_prefill(q, k, v, 0, tables, qs, seq, scale, max(n for _, n in spec),
-                                      _prefill_tiles(q_start, ctx))
+                                      _prefill_tiles(q_start, ctx), nt=nt)
     _close(out, ref, atol=2e-2)
 
 
