@@ -66,6 +66,7 @@ class EngineArgs:
     poll_every: int = 8
     async_mode: bool = False
     overlap_prefill: bool = False  # prefill on its own HIP stream, concurrent with decode bursts
+    precapture_graphs: bool = True  # capture every decode bucket at the first burst (and after FSM growth)
 
     @classmethod
     def from_configs(cls, model: str, backend: str, weights: Optional[str] = None,
@@ -85,7 +86,8 @@ class EngineArgs:
                    use_hip_graphs=ec.get("use_hip_graphs", True),
                    kv_cache_gb=ec.get("kv_cache_gb"),
                    honor_max_num_seqs=ec.get("honor_max_num_seqs", False),
-                   overlap_prefill=ec.get("overlap_prefill", False))
+                   overlap_prefill=ec.get("overlap_prefill", False),
+                   precapture_graphs=ec.get("precapture_graphs", True))
         dtype = ec.get("dtype", "bfloat16")
         args.dtype = getattr(torch, dtype) if isinstance(dtype, str) else dtype
         for key, value in kw.items():
