@@ -76,8 +76,11 @@ __device__ __forceinline__ void load_chunk(Chunk<HD>& c, const KVGeom& g, int bl
 }
 
 // Online-softmax update + O^T accumulation for one chunk starting at token t0.
-// visible(t) decides masking (t = absolute token index); n_valid bounds V reads.
-template <int HD, typename Vis>
+// visible(t) decides masking (t = absolute token index); kv_end bounds V reads.
+// MASKED = false: the caller guarantees every token of the chunk is visible to
+// every column (wave-uniform), so the per-token mask and the V-tail zeroing
+// (~60 VALU ops per chunk beside 16 MFMAs) are skipped.
+template <int HD, typename Vis, bool MASKED = true>
 __device__ __forceinline__ void compute_chunk(const Chunk<HD>& c, const bf16x8 (&bq)[HD / 32], int t0, int kv_end,
                                               Vis visible, float scale_log2, float& m, float& l,
                                               f32x4 (&o)[HD / 16], int lane) {
@@ -96,7 +99,7 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD>& c, const bf16x8 (
   for (int j = 0; j < 8; ++j) {
     const int t = t0 + 8 * h + j;
     const float sv = s[j >> 2][j & 3];
-    p[j] = (t < kv_end && visible(t)) ? sv * scale_log2 : -INFINITY;
+    p[j] = (!MASKED || (t < kv_end && visible(t))) ? sv * scale_log2 : -INFINITY;
     mx = fmaxf(mx, p[j]);
   }
   mx = fmaxf(mx, __shfl_xor(mx, 16, WAVE));
@@ -120,20 +123,28 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD>& c, const bf16x8 (
   for (int j = 0; j < 8; ++j) bp[j] = static_cast<__bf16>(p[j]);
   // tokens past kv_end may hold stale (even non-finite) bytes: zero their V
   // with branch-free 32-bit masks (a divergent branch here splits the vmcnt waits)
-  uint32_t keep[4];
+  if constexpr (MASKED) {
+    uint32_t keep[4];
 #pragma unroll
-  for (int j2 = 0; j2 < 4; ++j2) {
-    const int t = t0 + 8 * h + 2 * j2;
-    keep[j2] = (t < kv_end ? 0x0000ffffu : 0u) | (t + 1 < kv_end ? 0xffff0000u : 0u);
-  }
+    for (int j2 = 0; j2 < 4; ++j2) {
+      const int t = t0 + 8 * h + 2 * j2;
+      keep[j2] = (t < kv_end ? 0x0000ffffu : 0u) | (t + 1 < kv_end ? 0xffff0000u : 0u);
+    }
 #pragma unroll
-  for (int dt = 0; dt < HD / 16; ++dt) {
-    o[dt] *= alpha;
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 va = __builtin_bit_cast(u32x4, c.v[dt]);
+    for (int dt = 0; dt < HD / 16; ++dt) {
+      o[dt] *= alpha;
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 va = __builtin_bit_cast(u32x4, c.v[dt]);
 #pragma unroll
-    for (int j2 = 0; j2 < 4; ++j2) va[j2] &= keep[j2];
-    o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, va), bp, o[dt], 0, 0, 0);
+      for (int j2 = 0; j2 < 4; ++j2) va[j2] &= keep[j2];
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, va), bp, o[dt], 0, 0, 0);
+    }
+  } else {
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) {
+      o[dt] *= alpha;
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.v[dt], bp, o[dt], 0, 0, 0);
+    }
   }
 }
 
@@ -239,7 +250,10 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
       const int e0 = table[t0 / BS], e1 = table[min(t0 / BS + 1, last_blk)];
       Chunk<HD> c;
       load_chunk<HD, KT>(c, g, e0, e1, kvh, lane);
-      compute_chunk<HD>(c, bq, t0, ctx, AllVisible{}, scale_log2, m, l, o, lane);
+      if (t0 + CHUNK <= ctx)  // wave-uniform: a full chunk needs no tail masking
+        compute_chunk<HD, AllVisible, false>(c, bq, t0, ctx, AllVisible{}, scale_log2, m, l, o, lane);
+      else
+        compute_chunk<HD>(c, bq, t0, ctx, AllVisible{}, scale_log2, m, l, o, lane);
     }
 
     // combine the 4 waves through LDS
@@ -352,13 +366,15 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   bf16x8 bq[NT][HD / 32];
   float m[NT], l[NT];
   f32x4 o[NT][HD / 16];
-  int my_pos[NT], sub_end[NT];  // query position of this lane's column; exclusive key bound per sub-tile
+  // query position of this lane's column; per sub-tile: first row's position, exclusive key bound
+  int my_pos[NT], sub_first[NT], sub_end[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const int my_row = row0 + 16 * nt + r;
     const bool ok = my_row < q_end;
     load_q<HD>(bq[nt], q + (static_cast<size_t>(ok ? my_row : row0) * n_q + qh) * HD, ok, lane);
     my_pos[nt] = pos0 + (my_row - qs);
+    sub_first[nt] = pos0 + (row0 + 16 * nt - qs);
     sub_end[nt] = pos0 + (min(row0 + 16 * nt + 15, q_end - 1) - qs) + 1;
     m[nt] = -INFINITY;
     l[nt] = 0.f;
@@ -387,10 +403,15 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
     const int cn = min(c + 1, nchunk - 1);
     load_chunk<HD>(nxt, g, block_at(2 * cn), block_at(min(2 * cn + 1, nblk - 1)), kvh, lane);
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-      if (c * CHUNK < sub_end[nt])  // wave-uniform: skip chunks wholly in this sub-tile's causal future
+    for (int nt = 0; nt < NT; ++nt) {
+      if (c * CHUNK >= sub_end[nt]) continue;  // wave-uniform: chunk wholly in this sub-tile's causal future
+      if ((c + 1) * CHUNK <= sub_first[nt])     // wave-uniform: every key visible to every row
+        compute_chunk<HD, Causal, false>(cur, bq[nt], c * CHUNK, sub_end[nt], Causal{my_pos[nt]}, scale_log2,
+                                         m[nt], l[nt], o[nt], lane);
+      else
         compute_chunk<HD>(cur, bq[nt], c * CHUNK, sub_end[nt], Causal{my_pos[nt]}, scale_log2, m[nt], l[nt],
                           o[nt], lane);
+    }
     cur = nxt;
   }
 #pragma unroll
