@@ -233,15 +233,18 @@ class DecoderModel:
                 v_cache: torch.Tensor) -> torch.Tensor:
         """Returns logits ``[len(logits_idx) or B, vocab]`` (full vocab, fp32 or bf16)."""
         ops, c = self.ops, self.cfg
-        x = F.embedding(tokens.long(), self.embed)
-        residual = None
         fp8 = self.quant == "fp8"
+        residual = None
+        x = F.embedding(tokens.long(), self.embed) if fp8 else None
         for li, L in enumerate(self.layers):
             if fp8:  # norm + row-wise fp8 quant fused; hipBLASLt fp8 GEMM
                 hq, hs, residual = ops.add_rmsnorm_fp8(x, residual, L["ln1"], c.rms_eps)
                 qkv = ops.linear_fp8(hq, hs, L["qkv"], L["qkv_s"], L.get("qkv_bias"))
             else:
-                h, residual = ops.add_rmsnorm(x, residual, L["ln1"], c.rms_eps)
+                if li == 0:  # embedding gather fused with the first input norm
+                    h, residual = ops.embed_rmsnorm(tokens, self.embed, L["ln1"], c.rms_eps)
+                else:
+                    h, residual = ops.add_rmsnorm(x, residual, L["ln1"], c.rms_eps)
                 qkv = ops.linear(h, L["qkv"], L.get("qkv_bias"))
             q = ops.qk_norm_rope_kv_write(qkv, meta.positions, meta.slots, self.n_q, self.n_kv, self.hd,
                                           L.get("q_norm"), L.get("k_norm"), c.rms_eps, self.cos_sin,

@@ -26,6 +26,7 @@ def _torch_ops() -> SimpleNamespace:
         linear=torch.nn.functional.linear,
         rmsnorm=_ref.rmsnorm,
         add_rmsnorm=_ref.add_rmsnorm,
+        embed_rmsnorm=_ref.embed_rmsnorm,
         qk_norm_rope_kv_write=_ref.qk_norm_rope_kv_write,
         paged_attention_decode=decode,
         paged_attention_prefill=prefill,

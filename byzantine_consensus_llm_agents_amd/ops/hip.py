@@ -32,6 +32,7 @@ def load_library(path: str = None) -> ctypes.CDLL:
     sig = {
         "bcg_add_rmsnorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_int, c_void_p],
         "bcg_silu_mul": [c_void_p, c_void_p, c_int64, c_int, c_void_p],
+        "bcg_embed_rmsnorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
         "bcg_qk_norm_rope_kv_write": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                       c_float, c_void_p],
@@ -96,6 +97,18 @@ def hip_ops() -> SimpleNamespace:
         out = torch.empty_like(x)
         _check(lib.bcg_add_rmsnorm(_p(x), _p(residual), _p(w), _p(out), T, H, eps, int(has_res), _stream()),
                "add_rmsnorm")
+        return out, residual
+
+    def embed_rmsnorm(tokens, table, w, eps):
+        """(rmsnorm(table[tokens]) * w, table[tokens]) in one pass over the gathered rows."""
+        _req(tokens.dtype == torch.int32 and tokens.is_contiguous() and tokens.dim() == 1, "tokens int32 [T]")
+        _req(table.dtype == torch.bfloat16 and table.is_contiguous() and table.dim() == 2, "table bf16 [V,H]")
+        T, H = tokens.numel(), table.shape[1]
+        _req(w.shape == (H,) and w.dtype == torch.bfloat16, "embed_rmsnorm: weight [H] bf16")
+        residual = torch.empty(T, H, dtype=table.dtype, device=table.device)
+        out = torch.empty_like(residual)
+        _check(lib.bcg_embed_rmsnorm(_p(tokens), _p(table), _p(w), _p(residual), _p(out), T, H, eps, _stream()),
+               "embed_rmsnorm")
         return out, residual
 
     def rmsnorm(x, w, eps):
@@ -255,6 +268,7 @@ def hip_ops() -> SimpleNamespace:
 
     return SimpleNamespace(name="hip", linear=linear, quant_fp8=quant_fp8, add_rmsnorm_fp8=add_rmsnorm_fp8,
                            silu_mul_fp8=silu_mul_fp8, linear_fp8=linear_fp8, rmsnorm=rmsnorm, add_rmsnorm=add_rmsnorm, silu_mul=silu_mul,
+                           embed_rmsnorm=embed_rmsnorm,
                            qk_norm_rope_kv_write=qk_norm_rope_kv_write,
                            paged_attention_decode=paged_attention_decode,
                            paged_attention_prefill=paged_attention_prefill,

@@ -38,6 +38,13 @@ def add_rmsnorm(x: torch.Tensor, residual: Optional[torch.Tensor], w: torch.Tens
     return rmsnorm(residual, w, eps), residual
 
 
+def embed_rmsnorm(tokens: torch.Tensor, table: torch.Tensor, w: torch.Tensor,
+                  eps: float) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Embedding gather fused with the first RMSNorm: (rmsnorm(E[tokens]) * w, E[tokens])."""
+    residual = table.index_select(0, tokens.long())
+    return rmsnorm(residual, w, eps), residual
+
+
 def rope_cache(max_pos: int, head_dim: int, theta: float, device=None) -> torch.Tensor:
     """[max_pos, head_dim] fp32: first half cos, second half sin (neox layout)."""
     half = head_dim // 2

@@ -5,6 +5,10 @@
 // is read once and written twice (residual + normed) -- the HBM minimum for
 // the fused op.  Sum of squares: wave shuffle reduce, then 4 partials via LDS.
 //
+// embed_rmsnorm (K-EMB fused with layer 0's input norm): the same row kernel
+// reading row tokens[t] of the embedding table, so the embedding never makes
+// a separate HBM round trip: residual <- E[tok], out <- rmsnorm(E[tok]) * w.
+//
 // silu_mul: grid-stride over 8-element vectors of [T, 2I] -> [T, I].
 
 #include "common.h"
@@ -16,11 +20,12 @@ constexpr int MAX_CHUNK = 4;  // H <= 256 * 8 * 4 = 8192
 
 __global__ __launch_bounds__(NORM_THREADS) void add_rmsnorm_kernel(
     const bf16_t* __restrict__ x, bf16_t* __restrict__ residual, const bf16_t* __restrict__ w,
-    bf16_t* __restrict__ out, int H, float eps, int has_residual) {
+    bf16_t* __restrict__ out, int H, float eps, int has_residual, const int* __restrict__ gather) {
   const int row = blockIdx.x;
   const int tid = threadIdx.x;
   const int nvec = H / 8;
   const size_t base = static_cast<size_t>(row) * H;
+  if (gather) x += static_cast<size_t>(gather[row]) * H - base;  // x row = table row gather[row]
   float v[MAX_CHUNK][8];
   float ss = 0.f;
 #pragma unroll
@@ -91,7 +96,19 @@ BCG_API int bcg_add_rmsnorm(const void* x, void* residual, const void* w, void* 
   if (H % 8 != 0 || H > NORM_THREADS * 8 * MAX_CHUNK || T <= 0) return -2;
   hipLaunchKernelGGL(add_rmsnorm_kernel, dim3(T), dim3(NORM_THREADS), 0, stream,
                      static_cast<const bf16_t*>(x), static_cast<bf16_t*>(residual),
-                     static_cast<const bf16_t*>(w), static_cast<bf16_t*>(out), H, eps, has_residual);
+                     static_cast<const bf16_t*>(w), static_cast<bf16_t*>(out), H, eps, has_residual,
+                     static_cast<const int*>(nullptr));
+  return BCG_CHECK_LAUNCH();
+}
+
+// residual[t] <- table[tokens[t]]; out[t] <- rmsnorm(residual[t]) * w.  Token ids must be < vocab
+// (checked by the caller on the host side of every path that produces them).
+BCG_API int bcg_embed_rmsnorm(const int* tokens, const void* table, const void* w, void* residual, void* out,
+                              int T, int H, float eps, hipStream_t stream) {
+  if (H % 8 != 0 || H > NORM_THREADS * 8 * MAX_CHUNK || T <= 0) return -2;
+  hipLaunchKernelGGL(add_rmsnorm_kernel, dim3(T), dim3(NORM_THREADS), 0, stream,
+                     static_cast<const bf16_t*>(table), static_cast<bf16_t*>(residual),
+                     static_cast<const bf16_t*>(w), static_cast<bf16_t*>(out), H, eps, 0, tokens);
   return BCG_CHECK_LAUNCH();
 }
 

@@ -221,3 +221,15 @@ def test_linear_fp8(hip):
     y = hip.linear_fp8(xq, xs, wq, ws)
     y_ref = R.linear_fp8(xq, xs, wq, ws)
     _close(y, y_ref, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("V,H", [(151936, 5120), (32768, 6144), (151936, 896)])
+def test_embed_rmsnorm(hip, V, H):
+    torch.manual_seed(7)
+    table = torch.randn(V, H, device="cuda", dtype=torch.bfloat16)
+    w = (torch.rand(H, device="cuda") + 0.5).to(torch.bfloat16)
+    tokens = torch.randint(0, V, (53,), device="cuda", dtype=torch.int32)
+    y_ref, r_ref = R.embed_rmsnorm(tokens, table, w, 1e-6)
+    y, r = hip.embed_rmsnorm(tokens, table, w, 1e-6)
+    _close(r, r_ref, atol=0, rtol=0)
+    _close(y, y_ref, atol=2e-2)
