@@ -166,6 +166,7 @@ class InferenceEngine:
         self.prefill_stream = torch.cuda.Stream(self.device) if self.overlap else None
         self._inflight = None
         self._snap = None        # host copy of (done, gen_count, out_tokens) after the last burst
+        self._engine_errors = 0
         self._snap_buf = None
         if self.backend == "hip" and args.use_hip_graphs:
             from .graphs import DecodeGraphs
@@ -311,6 +312,12 @@ class InferenceEngine:
                 try:
                     self._iterate()
                 except BaseException as exc:  # fail every pending request loudly
+                    self._engine_errors += 1
+                    if self._engine_errors <= 3:  # callers may turn it into retries: say what it was
+                        import sys
+                        import traceback
+                        print(f"[engine] scheduler iteration failed ({self._engine_errors}):", file=sys.stderr)
+                        traceback.print_exc(file=sys.stderr)
                     self._fail_all(exc)
 
     def _fail_all(self, exc):

@@ -109,8 +109,8 @@ def tensor_parallel_group(tp: int, custom_allreduce: bool = False) -> TPGroup:
                 mine = pg
         _TP_GROUPS[tp] = mine
     custom = None
-    if (custom_allreduce and os.environ.get("BCG_CUSTOM_AR", "1") != "0"
-            and dist.get_backend(_TP_GROUPS[tp]) == "nccl"):
+    mode = os.environ.get("BCG_CUSTOM_AR", "1")  # 0 = RCCL only, force = also over gloo (1-GPU tests)
+    if custom_allreduce and mode != "0" and (mode == "force" or dist.get_backend(_TP_GROUPS[tp]) == "nccl"):
         if tp not in _CUSTOM_AR:
             from .custom_allreduce import XGMIAllReduce
             _CUSTOM_AR[tp] = XGMIAllReduce(_TP_GROUPS[tp])
