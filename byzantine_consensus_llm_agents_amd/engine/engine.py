@@ -189,7 +189,12 @@ class InferenceEngine:
             budget = int(a.kv_cache_gb * 2 ** 30)
         elif self.device.type == "cuda":
             free, total = torch.cuda.mem_get_info(self.device)
-            reserve = 6 * 2 ** 30 + 2 * a.prefill_chunk_tokens * (m.cfg.hidden_size + 2 * m.inter) * 2
+            # prefill activations of one chunk + the decode graphs' private pool (largest
+            # bucket: logits / sampler temporaries, MLP activations) + the shared split-K scratch
+            rows = min(a.max_batch_seqs, 768)
+            graphs = rows * (m.cfg.vocab_size * 8 + 8 * m.inter + 16 * m.cfg.hidden_size) * 2
+            reserve = (6 * 2 ** 30 + 2 * a.prefill_chunk_tokens * (m.cfg.hidden_size + 2 * m.inter) * 2
+                       + graphs + self._decode_ws_bytes())
             budget = int(min(free - reserve, total * a.gpu_memory_utilization - torch.cuda.memory_allocated(self.device)))
         else:
             budget = 256 * 2 ** 20
@@ -205,6 +210,15 @@ class InferenceEngine:
         self.num_blocks = num_blocks
         self.max_blocks_per_seq = (a.max_model_len + bs - 1) // bs
         self.kv_bytes = 2 * self.k_cache.numel() * self.k_cache.element_size()
+
+    def _decode_ws_bytes(self) -> int:
+        if not hasattr(self.ops, "decode_workspace_numel"):
+            return 0
+        from .graphs import MAX_ROWS
+        a, m = self.args, self.model
+        rows = min(MAX_ROWS, max(a.max_batch_seqs, 1))
+        max_blocks = (a.max_model_len + a.kv_block_size - 1) // a.kv_block_size
+        return 4 * self.ops.decode_workspace_numel(rows, m.n_q, m.hd, max_blocks, a.kv_block_size)
 
     def _load_tuned_gemms(self):
         """Load PyTorch TunableOp results for this model's decode GEMM shapes (lookups only).
@@ -243,6 +257,9 @@ class InferenceEngine:
             "done": torch.ones(cap, dtype=torch.int32, device=dev), "next_tokens": z(),
             "out_tokens": torch.zeros(cap, OUT_WIDTH, dtype=torch.int32, device=dev)}
         self.slots: List[Optional[_Request]] = [None] * cap
+        # one split-K scratch for every decode graph (they never run concurrently)
+        ws = self._decode_ws_bytes() // 4
+        self.decode_ws = torch.empty(ws, dtype=torch.float32, device=dev) if ws else None
 
     def _phys(self, blocks: List[int]) -> List[int]:
         return [b + 1 for b in blocks]  # manager ids are shifted past scratch block 0
@@ -655,7 +672,7 @@ class InferenceEngine:
         rows = torch.arange(pos.shape[0], device=pos.device)
         slots = st["block_tables"][rows, (pos // bs).long()] * bs + pos % bs
         return AttnMeta(positions=pos, slots=slots.to(torch.int32), block_tables=st["block_tables"],
-                        seq_lens=st["seq_lens"], decode=True)
+                        seq_lens=st["seq_lens"], decode=True, workspace=self.decode_ws)
 
     def decode_step(self, st: Dict[str, torch.Tensor]):
         """One full decode step (forward + guided sampling), graph-capturable."""

@@ -67,10 +67,11 @@ class DecodeGraphs:
 
     def capture_all(self, max_rows: int):
         """Capture every bucket up to `max_rows` now (idle rows are parked), so no
-        capture lands later in the middle of serving."""
-        for b in BUCKETS:
-            if b > max_rows:
-                break
+        capture lands later in the middle of serving.  Largest first: the graphs
+        share one private pool, and smaller captures then carve their
+        activations out of the blocks the largest one freed (ascending order
+        made every capture allocate fresh segments: 19.75 GiB for Qwen3-32B)."""
+        for b in sorted((b for b in BUCKETS if b <= max_rows), reverse=True):
             if b not in self.graphs:
                 self.graphs[b] = self._capture(b)
 

@@ -37,6 +37,7 @@ class AttnMeta:
     decode: bool = False
     logits_idx: Optional[torch.Tensor] = None  # rows whose logits are needed
     tiles: Optional[torch.Tensor] = None       # [n_tiles, 3] int32 prefill work list (HIP kernel)
+    workspace: Optional[torch.Tensor] = None   # decode split-K scratch shared by all graphs (HIP)
 
 
 class TPGroup:
@@ -251,7 +252,7 @@ class DecoderModel:
                                           k_cache, v_cache, li)
             if meta.decode:
                 attn = ops.paged_attention_decode(q, k_cache, v_cache, li, meta.block_tables,
-                                                  meta.seq_lens, self.scale)
+                                                  meta.seq_lens, self.scale, meta.workspace)
             else:
                 attn = ops.paged_attention_prefill(q, k_cache, v_cache, li, meta.block_tables,
                                                    meta.q_start, meta.seq_lens, self.scale, meta.max_q_len,

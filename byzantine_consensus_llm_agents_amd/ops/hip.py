@@ -138,7 +138,14 @@ def hip_ops() -> SimpleNamespace:
             n_q, n_kv, head_dim, NB, BS, eps, _stream()), "qk_norm_rope_kv_write")
         return q
 
-    def paged_attention_decode(q, k_cache, v_cache, layer, block_tables, seq_lens, scale):
+    def decode_workspace_numel(B, n_q, hd, max_blocks, block_size=16):
+        split = lib.bcg_decode_split_tokens(B, 0, max_blocks * block_size)
+        max_splits = (max_blocks * block_size + split - 1) // split
+        return B * n_q * max_splits * (hd + 2)
+
+    def paged_attention_decode(q, k_cache, v_cache, layer, block_tables, seq_lens, scale, workspace=None):
+        """`workspace`: optional fp32 split-K scratch of >= decode_workspace_numel(...) elements,
+        shared by every decode graph (it is dead between launches) instead of one per graph."""
         B, n_q, hd = q.shape
         L, NB, n_kv, BS, _ = k_cache.shape
         _req(q.is_contiguous() and block_tables.dtype == torch.int32 and block_tables.is_contiguous()
@@ -147,7 +154,13 @@ def hip_ops() -> SimpleNamespace:
         _req(B <= 1024, "decode attention: at most 1024 rows")
         split = lib.bcg_decode_split_tokens(B, n_kv, max_blocks * BS)
         max_splits = (max_blocks * BS + split - 1) // split
-        ws = torch.empty(B * n_q * max_splits * (hd + 2), dtype=torch.float32, device=q.device)
+        need = B * n_q * max_splits * (hd + 2)
+        if workspace is None:
+            ws = torch.empty(need, dtype=torch.float32, device=q.device)
+        else:
+            _req(workspace.dtype == torch.float32 and workspace.is_contiguous() and workspace.numel() >= need,
+                 "decode attention workspace too small")
+            ws = workspace
         out = torch.empty(B, n_q * hd, dtype=q.dtype, device=q.device)
         _check(lib.bcg_paged_attention_decode(
             _p(q), _p(k_cache), _p(v_cache), layer, NB, n_kv, _p(block_tables), max_blocks, _p(seq_lens),
@@ -271,6 +284,7 @@ def hip_ops() -> SimpleNamespace:
                            embed_rmsnorm=embed_rmsnorm,
                            qk_norm_rope_kv_write=qk_norm_rope_kv_write,
                            paged_attention_decode=paged_attention_decode,
+                           decode_workspace_numel=decode_workspace_numel,
                            paged_attention_prefill=paged_attention_prefill,
                            paged_attention_decode_exp=paged_attention_decode_exp, sample_step=sample_step,
                            library=lib)
