@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--backend", default="hip")
     ap.add_argument("--quantization", default=None, choices=["fp8"])
+    ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"],
+                    help="fp8 halves KV bytes (reduced precision: never used for the bf16 headline)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--overlap-prefill", action="store_true",
@@ -164,7 +166,8 @@ def main():
     C.VLLM_CONFIG["quantization"] = args.quantization
     C.ENGINE_CONFIG.update(backend=args.backend, budget_aware_json=True, seed=args.seed + rank // args.tp,
                            use_hip_graphs=not args.no_graphs, prefix_caching=not args.no_prefix_cache,
-                           overlap_prefill=args.overlap_prefill, custom_allreduce=not args.no_custom_allreduce)
+                           overlap_prefill=args.overlap_prefill, custom_allreduce=not args.no_custom_allreduce,
+                           kv_cache_dtype=args.kv_cache_dtype)
     C.BCG_CONFIG["value_range"] = (0, 50)
     random.seed(args.seed + rank)
 
@@ -232,6 +235,7 @@ def main():
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": "fp8" if args.quantization == "fp8" else "bf16",
+            "kv_cache_dtype": "fp8" if args.kv_cache_dtype == "fp8" else "bf16",
             "data": "synthetic (random-init weights, synthetic BPE tokenizer, budget-aware JSON grammar)",
             "config": {"model": model, "honest": args.honest, "byzantine": args.byzantine,
                        "global_batch": args.sims_per_gpu * (args.honest + args.byzantine) * (world // args.tp),

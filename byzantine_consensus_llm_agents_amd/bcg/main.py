@@ -41,6 +41,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--weights", type=str, default=None, help="'random' or a safetensors directory")
     p.add_argument("--quantization", type=str, default=None, choices=["fp8"],
                    help="fp8 (e4m3fn) projection GEMMs (the reference only logs this key)")
+    p.add_argument("--kv-cache-dtype", type=str, default=None, choices=["auto", "fp8"],
+                   help="KV cache element type: auto (= bf16) or fp8 (e4m3fn, half the bytes)")
     p.add_argument("--budget-aware-json", action="store_true",
                    help="Close the JSON before max_tokens instead of truncating")
     return p
@@ -61,6 +63,8 @@ def _apply_engine_flags(args):
         ENGINE_CONFIG["seed"] = args.seed
     if args.budget_aware_json:
         ENGINE_CONFIG["budget_aware_json"] = True
+    if args.kv_cache_dtype:
+        ENGINE_CONFIG["kv_cache_dtype"] = args.kv_cache_dtype
 
 
 def main(argv=None):

@@ -67,6 +67,7 @@ class EngineArgs:
     async_mode: bool = False
     overlap_prefill: bool = False  # prefill on its own HIP stream, concurrent with decode bursts
     precapture_graphs: bool = True  # capture every decode bucket at the first burst (and after FSM growth)
+    kv_cache_dtype: str = "auto"    # "auto" = activation dtype (bf16); "fp8" = OCP e4m3fn (half the KV bytes)
 
     @classmethod
     def from_configs(cls, model: str, backend: str, weights: Optional[str] = None,
@@ -87,7 +88,8 @@ class EngineArgs:
                    kv_cache_gb=ec.get("kv_cache_gb"),
                    honor_max_num_seqs=ec.get("honor_max_num_seqs", False),
                    overlap_prefill=ec.get("overlap_prefill", False),
-                   precapture_graphs=ec.get("precapture_graphs", True))
+                   precapture_graphs=ec.get("precapture_graphs", True),
+                   kv_cache_dtype=ec.get("kv_cache_dtype", "auto"))
         dtype = ec.get("dtype", "bfloat16")
         args.dtype = getattr(torch, dtype) if isinstance(dtype, str) else dtype
         for key, value in kw.items():
@@ -180,10 +182,19 @@ class InferenceEngine:
         return tensor_parallel_group(tp_size, custom_allreduce=(
             self.backend == "hip" and ENGINE_CONFIG.get("custom_allreduce", True)))
 
+    def kv_dtype(self) -> torch.dtype:
+        kd = (self.args.kv_cache_dtype or "auto").lower()
+        if kd == "auto":
+            return self.args.dtype
+        if kd in ("fp8", "fp8_e4m3", "float8_e4m3fn"):
+            return torch.float8_e4m3fn
+        raise ValueError(f"unsupported kv_cache_dtype {self.args.kv_cache_dtype!r} (auto | fp8)")
+
     def _alloc_kv_cache(self):
         a, m = self.args, self.model
         bs = a.kv_block_size
-        per_block = 2 * m.cfg.num_layers * m.n_kv * bs * m.hd * torch.tensor([], dtype=a.dtype).element_size()
+        kv_dtype = self.kv_dtype()
+        per_block = 2 * m.cfg.num_layers * m.n_kv * bs * m.hd * torch.tensor([], dtype=kv_dtype).element_size()
         want_tokens = a.max_batch_seqs * a.max_model_len
         if a.kv_cache_gb:
             budget = int(a.kv_cache_gb * 2 ** 30)
@@ -199,10 +210,10 @@ class InferenceEngine:
         else:
             budget = 256 * 2 ** 20
         num_blocks = max(16, min(budget // per_block, want_tokens // bs + 1))
-        self.k_cache = torch.zeros((m.cfg.num_layers, num_blocks, m.n_kv, bs, m.hd), dtype=a.dtype,
+        self.k_cache = torch.zeros((m.cfg.num_layers, num_blocks, m.n_kv, bs, m.hd), dtype=kv_dtype,
                                    device=self.device)
         # V is stored transposed per block-head (see ops/reference.py)
-        self.v_cache = torch.zeros((m.cfg.num_layers, num_blocks, m.n_kv, m.hd, bs), dtype=a.dtype,
+        self.v_cache = torch.zeros((m.cfg.num_layers, num_blocks, m.n_kv, m.hd, bs), dtype=kv_dtype,
                                    device=self.device)
         from ..runtime import BlockManager
         # block 0 is scratch (padding rows of graph buckets write there); never handed out

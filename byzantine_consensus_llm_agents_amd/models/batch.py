@@ -12,11 +12,12 @@ import torch
 from .transformer import AttnMeta, DecoderModel
 
 
-def alloc_kv(model: DecoderModel, num_blocks: int, block_size: int = 16, device=None):
+def alloc_kv(model: DecoderModel, num_blocks: int, block_size: int = 16, device=None, dtype=None):
     dev = device or model.device
     c = model.cfg
-    k = torch.zeros(c.num_layers, num_blocks, model.n_kv, block_size, model.hd, dtype=model.dtype, device=dev)
-    v = torch.zeros(c.num_layers, num_blocks, model.n_kv, model.hd, block_size, dtype=model.dtype, device=dev)
+    dt = dtype or model.dtype
+    k = torch.zeros(c.num_layers, num_blocks, model.n_kv, block_size, model.hd, dtype=dt, device=dev)
+    v = torch.zeros(c.num_layers, num_blocks, model.n_kv, model.hd, block_size, dtype=dt, device=dev)
     return k, v
 
 

@@ -35,13 +35,13 @@ def load_library(path: str = None) -> ctypes.CDLL:
         "bcg_embed_rmsnorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
         "bcg_qk_norm_rope_kv_write": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                                      c_float, c_void_p],
+                                      c_float, c_int, c_void_p],
         "bcg_paged_attention_decode": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                        c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int,
-                                       c_int, c_void_p, c_void_p],
+                                       c_int, c_void_p, c_int, c_void_p],
         "bcg_paged_attention_prefill": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
-                                        c_void_p, c_int, c_void_p],
+                                        c_void_p, c_int, c_int, c_void_p],
         "bcg_decode_split_tokens": [c_int, c_int, c_int],
         "bcg_paged_attention_decode_exp": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                            c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int, c_int,
@@ -80,6 +80,13 @@ def _check(rc: int, name: str):
 def _req(cond: bool, msg: str):
     if not cond:
         raise ValueError(msg)
+
+
+def _kv_fp8(k_cache: torch.Tensor, v_cache: torch.Tensor) -> int:
+    """1 for an fp8 (e4m3fn) KV cache, 0 for bf16; anything else is refused before launch."""
+    _req(k_cache.dtype == v_cache.dtype and k_cache.dtype in (torch.bfloat16, torch.float8_e4m3fn)
+         and k_cache.is_contiguous() and v_cache.is_contiguous(), "KV cache: contiguous bf16 or float8_e4m3fn")
+    return int(k_cache.dtype == torch.float8_e4m3fn)
 
 
 def hip_ops() -> SimpleNamespace:
@@ -135,7 +142,7 @@ def hip_ops() -> SimpleNamespace:
         _check(lib.bcg_qk_norm_rope_kv_write(
             _p(qkv), _p(positions), _p(slots), _p(q), _p(q_norm) if q_norm is not None else None,
             _p(k_norm) if k_norm is not None else None, _p(cos_sin), _p(k_cache), _p(v_cache), layer, T,
-            n_q, n_kv, head_dim, NB, BS, eps, _stream()), "qk_norm_rope_kv_write")
+            n_q, n_kv, head_dim, NB, BS, eps, _kv_fp8(k_cache, v_cache), _stream()), "qk_norm_rope_kv_write")
         return q
 
     def decode_workspace_numel(B, n_q, hd, max_blocks, block_size=16):
@@ -164,7 +171,8 @@ def hip_ops() -> SimpleNamespace:
         out = torch.empty(B, n_q * hd, dtype=q.dtype, device=q.device)
         _check(lib.bcg_paged_attention_decode(
             _p(q), _p(k_cache), _p(v_cache), layer, NB, n_kv, _p(block_tables), max_blocks, _p(seq_lens),
-            B, n_q, hd, BS, scale, _p(ws), max_splits, split, _p(out), _stream()), "paged_attention_decode")
+            B, n_q, hd, BS, scale, _p(ws), max_splits, split, _p(out), _kv_fp8(k_cache, v_cache), _stream()),
+            "paged_attention_decode")
         return out
 
     def paged_attention_decode_exp(q, k_cache, v_cache, layer, block_tables, seq_lens, scale, variant):
@@ -194,7 +202,7 @@ def hip_ops() -> SimpleNamespace:
         _check(lib.bcg_paged_attention_prefill(
             _p(q), _p(k_cache), _p(v_cache), layer, NB, n_kv, _p(block_tables), block_tables.shape[1],
             _p(q_start), _p(seq_lens), _p(tiles), tiles.shape[0], n_q, hd, BS, scale, _p(out),
-            nt or prefill_nt, _stream()), "paged_attention_prefill")
+            nt or prefill_nt, _kv_fp8(k_cache, v_cache), _stream()), "paged_attention_prefill")
         return out
 
     use_skinny = os.environ.get("BCG_SKINNY_GEMM", "0") == "1"  # hipBLASLt wins (bench_ops r1)

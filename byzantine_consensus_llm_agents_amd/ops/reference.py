@@ -81,6 +81,8 @@ def qk_norm_rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, slots: tor
     bs = k_cache.shape[3]
     blk = (slots // bs).long()
     off = (slots % bs).long()
+    if k_cache.dtype == torch.float8_e4m3fn:  # fp8 KV cache: saturate (e4m3fn has no inf)
+        k, v = k.clamp(-448.0, 448.0), v.float().clamp(-448.0, 448.0)
     k_cache[layer, blk, :, off] = k.to(k_cache.dtype)
     v_cache[layer, blk, :, :, off] = v.to(v_cache.dtype)
     return q.to(qkv.dtype)

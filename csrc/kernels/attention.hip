@@ -26,6 +26,7 @@
 // head), causal over cached prefix + new tokens, varlen via a tile table.
 
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 
@@ -47,29 +48,50 @@ __device__ __forceinline__ size_t block_base(const KVGeom& g, int blk, int kvh) 
   return ((static_cast<size_t>(g.layer) * g.num_blocks + blk) * g.n_kv + kvh) * (BS * HD);
 }
 
-template <int HD>
+// A chunk's operands as loaded: bf16x8 (16 B) per fragment, or -- fp8 KV cache --
+// the raw 8 e4m3fn bytes, widened to bf16 only right before their MFMA so the
+// loads of the next chunk stay in flight (converting at load time would wait).
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+template <int HD, bool F8 = false>
 struct Chunk {
-  bf16x8 k[2][HD / 32];   // S^T A-operands, tile u, k-step kk
-  bf16x8 v[HD / 16];      // O^T A-operands, d-tile dt
+  typedef typename std::conditional<F8, u32x2, bf16x8>::type E;
+  E k[2][HD / 32];   // S^T A-operands, tile u, k-step kk
+  E v[HD / 16];      // O^T A-operands, d-tile dt
 };
 
+__device__ __forceinline__ bf16x8 to_bf16x8(const bf16x8& x) { return x; }
+
+__device__ __forceinline__ bf16x8 to_bf16x8(const u32x2& x) {  // 8 x e4m3fn -> 8 x bf16 (exact)
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const bf16x2 a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(x[0], 1.f, false);
+  const bf16x2 b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(x[0], 1.f, true);
+  const bf16x2 c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(x[1], 1.f, false);
+  const bf16x2 d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(x[1], 1.f, true);
+  return bf16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
+
 // Issue every load of one 32-token chunk whose blocks are blk0/blk1.
-template <int HD, bool KT = false>
-__device__ __forceinline__ void load_chunk(Chunk<HD>& c, const KVGeom& g, int blk0, int blk1, int kvh, int lane) {
+template <int HD, bool KT = false, bool F8 = false>
+__device__ __forceinline__ void load_chunk(Chunk<HD, F8>& c, const KVGeom& g, int blk0, int blk1, int kvh,
+                                           int lane) {
+  typedef typename Chunk<HD, F8>::E E;
+  typedef typename std::conditional<F8, uint8_t, bf16_t>::type T;  // cache element
+  const T* kc = reinterpret_cast<const T*>(g.k);
+  const T* vc = reinterpret_cast<const T*>(g.v);
   const int r = lane & 15, h = lane >> 4;
   const size_t b0 = block_base<HD>(g, blk0, kvh), b1 = block_base<HD>(g, blk1, kvh);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int t = 8 * (r >> 2) + 4 * u + (r & 3);
     // KT: K block-head stored [HD/32][BS][32] -> each load instruction reads 256-B runs
-    const bf16_t* krow = g.k + (t < BS ? b0 : b1) + (KT ? (t & (BS - 1)) * 32 : (t & (BS - 1)) * HD) + 8 * h;
+    const T* krow = kc + (t < BS ? b0 : b1) + (KT ? (t & (BS - 1)) * 32 : (t & (BS - 1)) * HD) + 8 * h;
 #pragma unroll
-    for (int kk = 0; kk < HD / 32; ++kk)
-      c.k[u][kk] = *reinterpret_cast<const bf16x8*>(krow + kk * (KT ? BS * 32 : 32));
+    for (int kk = 0; kk < HD / 32; ++kk) c.k[u][kk] = *reinterpret_cast<const E*>(krow + kk * (KT ? BS * 32 : 32));
   }
-  const bf16_t* vb = g.v + (h < 2 ? b0 : b1) + 8 * (h & 1);
+  const T* vb = vc + (h < 2 ? b0 : b1) + 8 * (h & 1);
 #pragma unroll
-  for (int dt = 0; dt < HD / 16; ++dt) c.v[dt] = *reinterpret_cast<const bf16x8*>(vb + (dt * 16 + r) * BS);
+  for (int dt = 0; dt < HD / 16; ++dt) c.v[dt] = *reinterpret_cast<const E*>(vb + (dt * 16 + r) * BS);
   // Keep all 16 loads of the chunk together: without this fence hipcc sinks the
   // V loads below the S^T MFMAs that wait for K, i.e. two serial HBM round trips.
   __builtin_amdgcn_sched_barrier(0);
@@ -80,8 +102,8 @@ __device__ __forceinline__ void load_chunk(Chunk<HD>& c, const KVGeom& g, int bl
 // MASKED = false: the caller guarantees every token of the chunk is visible to
 // every column (wave-uniform), so the per-token mask and the V-tail zeroing
 // (~60 VALU ops per chunk beside 16 MFMAs) are skipped.
-template <int HD, typename Vis, bool MASKED = true>
-__device__ __forceinline__ void compute_chunk(const Chunk<HD>& c, const bf16x8 (&bq)[HD / 32], int t0, int kv_end,
+template <int HD, typename Vis, bool MASKED = true, bool F8 = false>
+__device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16x8 (&bq)[HD / 32], int t0, int kv_end,
                                               Vis visible, float scale_log2, float& m, float& l,
                                               f32x4 (&o)[HD / 16], int lane) {
   const int h = lane >> 4;
@@ -91,7 +113,7 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD>& c, const bf16x8 (
     s[u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < HD / 32; ++kk)
-      s[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.k[u][kk], bq[kk], s[u], 0, 0, 0);
+      s[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(to_bf16x8(c.k[u][kk]), bq[kk], s[u], 0, 0, 0);
   }
   float p[8];
   float mx = -INFINITY;
@@ -134,7 +156,7 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD>& c, const bf16x8 (
     for (int dt = 0; dt < HD / 16; ++dt) {
       o[dt] *= alpha;
       typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      u32x4 va = __builtin_bit_cast(u32x4, c.v[dt]);
+      u32x4 va = __builtin_bit_cast(u32x4, to_bf16x8(c.v[dt]));
 #pragma unroll
       for (int j2 = 0; j2 < 4; ++j2) va[j2] &= keep[j2];
       o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, va), bp, o[dt], 0, 0, 0);
@@ -143,7 +165,7 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD>& c, const bf16x8 (
 #pragma unroll
     for (int dt = 0; dt < HD / 16; ++dt) {
       o[dt] *= alpha;
-      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c.v[dt], bp, o[dt], 0, 0, 0);
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(to_bf16x8(c.v[dt]), bp, o[dt], 0, 0, 0);
     }
   }
 }
@@ -181,7 +203,7 @@ struct Causal {
 constexpr int DEC_SPLIT = DEC_WAVES * CHUNK;  // 128 tokens per item
 constexpr int DEC_MAX_B = 1024;
 
-template <int HD, bool KT = false>
+template <int HD, bool KT = false, bool F8 = false>
 __global__ __launch_bounds__(256) void decode_attn_kernel(
     const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
     const int* __restrict__ seq_lens, int B, int n_q, float scale_log2, float* __restrict__ part_o,
@@ -248,12 +270,12 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
     if (t0 < ctx) {  // wave-uniform
       const int last_blk = (ctx - 1) / BS;
       const int e0 = table[t0 / BS], e1 = table[min(t0 / BS + 1, last_blk)];
-      Chunk<HD> c;
-      load_chunk<HD, KT>(c, g, e0, e1, kvh, lane);
+      Chunk<HD, F8> c;
+      load_chunk<HD, KT, F8>(c, g, e0, e1, kvh, lane);
       if (t0 + CHUNK <= ctx)  // wave-uniform: a full chunk needs no tail masking
-        compute_chunk<HD, AllVisible, false>(c, bq, t0, ctx, AllVisible{}, scale_log2, m, l, o, lane);
+        compute_chunk<HD, AllVisible, false, F8>(c, bq, t0, ctx, AllVisible{}, scale_log2, m, l, o, lane);
       else
-        compute_chunk<HD>(c, bq, t0, ctx, AllVisible{}, scale_log2, m, l, o, lane);
+        compute_chunk<HD, AllVisible, true, F8>(c, bq, t0, ctx, AllVisible{}, scale_log2, m, l, o, lane);
     }
 
     // combine the 4 waves through LDS
@@ -312,7 +334,7 @@ __global__ __launch_bounds__(HD) void decode_combine_kernel(const float* __restr
   out[static_cast<size_t>(bq) * HD + d] = f2bf(ll > 0.f ? oo / ll : 0.f);
 }
 
-template <int HD, bool KT = false>
+template <int HD, bool KT = false, bool F8 = false>
 void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks, const int* seq_lens, int B,
                    int n_q, float sl, float* ws, int max_splits, bf16_t* out, hipStream_t stream) {
   float* part_o = ws;
@@ -323,11 +345,11 @@ void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
     int per_cu = 0, cus = 0, dev = 0;
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_attn_kernel<HD, KT>, 256, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_attn_kernel<HD, KT, F8>, 256, 0);
     resident = std::max(1, per_cu) * std::max(1, cus);
   }
   const int grid = static_cast<int>(std::min<long>(static_cast<long>(B) * g.n_kv * max_splits, resident));
-  hipLaunchKernelGGL((decode_attn_kernel<HD, KT>), dim3(grid), dim3(256), 0, stream, q, g, tables, max_blocks,
+  hipLaunchKernelGGL((decode_attn_kernel<HD, KT, F8>), dim3(grid), dim3(256), 0, stream, q, g, tables, max_blocks,
                      seq_lens, B, n_q, sl, part_o, part_ml, max_splits);
   hipLaunchKernelGGL(decode_combine_kernel<HD>, dim3(B * n_q), dim3(HD), 0, stream, part_o, part_ml, seq_lens,
                      n_q, max_splits, DEC_SPLIT, out);
@@ -342,7 +364,7 @@ void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
 // K/V once for all of them: every 16-B K/V load feeds NT times the MFMAs of
 // the one-tile (NT = 1) form, which was load-bound (L2 -> CU) at 120-200 TF/s.
 // Waves of a block: 4/NT row groups x NT heads; grid = (tiles, ceil(n_q/NT)).
-template <int HD, int NT>
+template <int HD, int NT, bool F8 = false>
 __global__ __launch_bounds__(256) void prefill_attn_kernel(
     const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
     const int* __restrict__ q_start, const int* __restrict__ seq_lens, const int* __restrict__ tiles,
@@ -397,20 +419,20 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   };
   // next-chunk loads issued unconditionally (clamped to the last chunk) -- see decode
   const int nchunk = (kv_end + CHUNK - 1) / CHUNK;
-  Chunk<HD> cur, nxt;
-  load_chunk<HD>(cur, g, block_at(0), block_at(min(1, nblk - 1)), kvh, lane);
+  Chunk<HD, F8> cur, nxt;
+  load_chunk<HD, false, F8>(cur, g, block_at(0), block_at(min(1, nblk - 1)), kvh, lane);
   for (int c = 0; c < nchunk; ++c) {
     const int cn = min(c + 1, nchunk - 1);
-    load_chunk<HD>(nxt, g, block_at(2 * cn), block_at(min(2 * cn + 1, nblk - 1)), kvh, lane);
+    load_chunk<HD, false, F8>(nxt, g, block_at(2 * cn), block_at(min(2 * cn + 1, nblk - 1)), kvh, lane);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       if (c * CHUNK >= sub_end[nt]) continue;  // wave-uniform: chunk wholly in this sub-tile's causal future
       if ((c + 1) * CHUNK <= sub_first[nt])     // wave-uniform: every key visible to every row
-        compute_chunk<HD, Causal, false>(cur, bq[nt], c * CHUNK, sub_end[nt], Causal{my_pos[nt]}, scale_log2,
-                                         m[nt], l[nt], o[nt], lane);
+        compute_chunk<HD, Causal, false, F8>(cur, bq[nt], c * CHUNK, sub_end[nt], Causal{my_pos[nt]},
+                                             scale_log2, m[nt], l[nt], o[nt], lane);
       else
-        compute_chunk<HD>(cur, bq[nt], c * CHUNK, sub_end[nt], Causal{my_pos[nt]}, scale_log2, m[nt], l[nt],
-                          o[nt], lane);
+        compute_chunk<HD, Causal, true, F8>(cur, bq[nt], c * CHUNK, sub_end[nt], Causal{my_pos[nt]},
+                                            scale_log2, m[nt], l[nt], o[nt], lane);
     }
     cur = nxt;
   }
@@ -431,22 +453,22 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   }
 }
 
-template <int HD>
+template <int HD, bool F8>
 int launch_prefill(int nt, int n_tiles, int n_q, const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
                    const int* q_start, const int* seq_lens, const int* tiles, float sl, bf16_t* out,
                    hipStream_t stream) {
   switch (nt) {
     case 1:
-      hipLaunchKernelGGL((prefill_attn_kernel<HD, 1>), dim3(n_tiles, n_q), dim3(256), 0, stream, q, g, tables,
+      hipLaunchKernelGGL((prefill_attn_kernel<HD, 1, F8>), dim3(n_tiles, n_q), dim3(256), 0, stream, q, g, tables,
                          max_blocks, q_start, seq_lens, tiles, n_q, sl, out);
       break;
     case 2:
-      hipLaunchKernelGGL((prefill_attn_kernel<HD, 2>), dim3(n_tiles, (n_q + 1) / 2), dim3(256), 0, stream, q, g,
-                         tables, max_blocks, q_start, seq_lens, tiles, n_q, sl, out);
+      hipLaunchKernelGGL((prefill_attn_kernel<HD, 2, F8>), dim3(n_tiles, (n_q + 1) / 2), dim3(256), 0, stream, q,
+                         g, tables, max_blocks, q_start, seq_lens, tiles, n_q, sl, out);
       break;
     case 4:
-      hipLaunchKernelGGL((prefill_attn_kernel<HD, 4>), dim3(n_tiles, (n_q + 3) / 4), dim3(256), 0, stream, q, g,
-                         tables, max_blocks, q_start, seq_lens, tiles, n_q, sl, out);
+      hipLaunchKernelGGL((prefill_attn_kernel<HD, 4, F8>), dim3(n_tiles, (n_q + 3) / 4), dim3(256), 0, stream, q,
+                         g, tables, max_blocks, q_start, seq_lens, tiles, n_q, sl, out);
       break;
     default:
       return -2;
@@ -463,19 +485,26 @@ int launch_prefill(int nt, int n_tiles, int n_q, const bf16_t* q, KVGeom g, cons
 // per CU at 3 waves/SIMD.
 BCG_API int bcg_decode_split_tokens(int B, int n_kv, int max_tokens) { return DEC_SPLIT; }
 
+// kv_fp8: the caches hold OCP e4m3fn bytes (scale 1) instead of bf16.
 BCG_API int bcg_paged_attention_decode(const void* q, const void* k_cache, const void* v_cache, int layer,
                                        int num_blocks, int n_kv, const int* block_tables, int max_blocks,
                                        const int* seq_lens, int B, int n_q, int hd, int block_size,
                                        float scale, float* workspace, int max_splits, int split_tokens,
-                                       void* out, hipStream_t stream) {
+                                       void* out, int kv_fp8, hipStream_t stream) {
   if (block_size != BS || n_q % n_kv || n_q / n_kv > 16 || B <= 0 || B > DEC_MAX_B) return -2;
   if (split_tokens != DEC_SPLIT || max_splits * split_tokens < max_blocks * BS) return -3;
   KVGeom g{static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), layer, num_blocks, n_kv};
   const bf16_t* qb = static_cast<const bf16_t*>(q);
   bf16_t* ob = static_cast<bf16_t*>(out);
   const float sl = scale * LOG2E;
-  if (hd == 128) {
+  if (hd == 128 && kv_fp8) {
+    launch_decode<128, false, true>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace, max_splits,
+                                    ob, stream);
+  } else if (hd == 128) {
     launch_decode<128>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace, max_splits, ob, stream);
+  } else if (hd == 64 && kv_fp8) {
+    launch_decode<64, false, true>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace, max_splits,
+                                   ob, stream);
   } else if (hd == 64) {
     launch_decode<64>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace, max_splits, ob, stream);
   } else {
@@ -508,7 +537,7 @@ BCG_API int bcg_paged_attention_prefill(const void* q, const void* k_cache, cons
                                         int num_blocks, int n_kv, const int* block_tables, int max_blocks,
                                         const int* q_start, const int* seq_lens, const int* tiles, int n_tiles,
                                         int n_q, int hd, int block_size, float scale, void* out, int nt,
-                                        hipStream_t stream) {
+                                        int kv_fp8, hipStream_t stream) {
   if (block_size != BS || n_q % n_kv || n_tiles <= 0) return -2;
   KVGeom g{static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), layer, num_blocks, n_kv};
   const float sl = scale * LOG2E;
@@ -516,11 +545,15 @@ BCG_API int bcg_paged_attention_prefill(const void* q, const void* k_cache, cons
   bf16_t* ob = static_cast<bf16_t*>(out);
   int rc;
   if (hd == 128)
-    rc = launch_prefill<128>(nt, n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens, tiles, sl, ob,
-                             stream);
+    rc = kv_fp8 ? launch_prefill<128, true>(nt, n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens,
+                                            tiles, sl, ob, stream)
+                : launch_prefill<128, false>(nt, n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens,
+                                             tiles, sl, ob, stream);
   else if (hd == 64)
-    rc = launch_prefill<64>(nt, n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens, tiles, sl, ob,
-                            stream);
+    rc = kv_fp8 ? launch_prefill<64, true>(nt, n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens,
+                                           tiles, sl, ob, stream)
+                : launch_prefill<64, false>(nt, n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens,
+                                            tiles, sl, ob, stream);
   else
     return -2;
   return rc ? rc : BCG_CHECK_LAUNCH();

@@ -9,6 +9,8 @@
 // KV cache layouts (see ops/reference.py):
 //   K: [L, NB, n_kv, BS, hd]   (token rows: the A operand of S^T = K Q^T)
 //   V: [L, NB, n_kv, hd, BS]   (transposed: the A operand of O^T = V^T P^T)
+// Element type: bf16, or OCP fp8 e4m3fn (kv_fp8; scale 1, saturated to
+// +-448, round-to-nearest-even) -- half the KV bytes every decode step streams.
 
 #include "common.h"
 
@@ -16,10 +18,21 @@ namespace {
 
 constexpr int HEADS_PER_BLOCK = 4;  // 4 waves per 256-thread workgroup
 
+template <typename T>
+__device__ __forceinline__ T to_cache(float f);
+template <>
+__device__ __forceinline__ bf16_t to_cache<bf16_t>(float f) { return f2bf(f); }
+template <>
+__device__ __forceinline__ uint8_t to_cache<uint8_t>(float f) {
+  f = fminf(fmaxf(f, -448.f), 448.f);  // e4m3fn has no inf: saturate
+  return static_cast<uint8_t>(__builtin_amdgcn_cvt_pk_fp8_f32(f, 0.f, 0, false) & 0xff);
+}
+
+template <typename CacheT>
 __global__ __launch_bounds__(256) void qk_norm_rope_kv_kernel(
     const bf16_t* __restrict__ qkv, const int* __restrict__ positions, const int* __restrict__ slots,
     bf16_t* __restrict__ q_out, const bf16_t* __restrict__ q_norm, const bf16_t* __restrict__ k_norm,
-    const float* __restrict__ cos_sin, bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
+    const float* __restrict__ cos_sin, CacheT* __restrict__ k_cache, CacheT* __restrict__ v_cache,
     int layer, int T, int n_q, int n_kv, int hd, int num_blocks, int block_size, float eps) {
   const int lane = threadIdx.x & 63;
   const int slot_head = blockIdx.y * HEADS_PER_BLOCK + (threadIdx.x >> 6);
@@ -40,8 +53,8 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kv_kernel(
     const int h = slot_head - n_q - n_kv;
     const size_t vbase = ((static_cast<size_t>(layer) * num_blocks + blk) * n_kv + h) * hd * block_size;
     if (active) {
-      v_cache[vbase + static_cast<size_t>(lane) * block_size + off] = src[lane];
-      v_cache[vbase + static_cast<size_t>(lane + half) * block_size + off] = src[lane + half];
+      v_cache[vbase + static_cast<size_t>(lane) * block_size + off] = to_cache<CacheT>(x1);
+      v_cache[vbase + static_cast<size_t>(lane + half) * block_size + off] = to_cache<CacheT>(x2);
     }
     return;
   }
@@ -66,9 +79,9 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kv_kernel(
     dst[lane + half] = f2bf(y2);
   } else {
     const int h = slot_head - n_q;
-    bf16_t* dst = k_cache + (((static_cast<size_t>(layer) * num_blocks + blk) * n_kv + h) * block_size + off) * hd;
-    dst[lane] = f2bf(y1);
-    dst[lane + half] = f2bf(y2);
+    CacheT* dst = k_cache + (((static_cast<size_t>(layer) * num_blocks + blk) * n_kv + h) * block_size + off) * hd;
+    dst[lane] = to_cache<CacheT>(y1);
+    dst[lane + half] = to_cache<CacheT>(y2);
   }
 }
 
@@ -77,13 +90,22 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kv_kernel(
 BCG_API int bcg_qk_norm_rope_kv_write(const void* qkv, const int* positions, const int* slots, void* q_out,
                                       const void* q_norm, const void* k_norm, const float* cos_sin,
                                       void* k_cache, void* v_cache, int layer, int T, int n_q, int n_kv,
-                                      int hd, int num_blocks, int block_size, float eps, hipStream_t stream) {
+                                      int hd, int num_blocks, int block_size, float eps, int kv_fp8,
+                                      hipStream_t stream) {
   if (hd > 128 || (hd & 1) || T <= 0) return -2;
   const int n_heads = n_q + 2 * n_kv;
   dim3 grid(T, (n_heads + HEADS_PER_BLOCK - 1) / HEADS_PER_BLOCK);
-  hipLaunchKernelGGL(qk_norm_rope_kv_kernel, grid, dim3(256), 0, stream, static_cast<const bf16_t*>(qkv),
-                     positions, slots, static_cast<bf16_t*>(q_out), static_cast<const bf16_t*>(q_norm),
-                     static_cast<const bf16_t*>(k_norm), cos_sin, static_cast<bf16_t*>(k_cache),
-                     static_cast<bf16_t*>(v_cache), layer, T, n_q, n_kv, hd, num_blocks, block_size, eps);
+  if (kv_fp8)
+    hipLaunchKernelGGL(qk_norm_rope_kv_kernel<uint8_t>, grid, dim3(256), 0, stream,
+                       static_cast<const bf16_t*>(qkv), positions, slots, static_cast<bf16_t*>(q_out),
+                       static_cast<const bf16_t*>(q_norm), static_cast<const bf16_t*>(k_norm), cos_sin,
+                       static_cast<uint8_t*>(k_cache), static_cast<uint8_t*>(v_cache), layer, T, n_q, n_kv, hd,
+                       num_blocks, block_size, eps);
+  else
+    hipLaunchKernelGGL(qk_norm_rope_kv_kernel<bf16_t>, grid, dim3(256), 0, stream,
+                       static_cast<const bf16_t*>(qkv), positions, slots, static_cast<bf16_t*>(q_out),
+                       static_cast<const bf16_t*>(q_norm), static_cast<const bf16_t*>(k_norm), cos_sin,
+                       static_cast<bf16_t*>(k_cache), static_cast<bf16_t*>(v_cache), layer, T, n_q, n_kv, hd,
+                       num_blocks, block_size, eps);
   return BCG_CHECK_LAUNCH();
 }

@@ -97,3 +97,22 @@ def test_chunked_prefill_matches_single_chunk(llm):
     finally:
         eng.args.prefill_chunk_tokens, eng.args.prefix_caching = saved
     assert got == ref
+
+
+def test_engine_fp8_kv_cache_cpu(fresh_engine_state):
+    """kv_cache_dtype=fp8: e4m3fn caches end to end on the reference ops; guided JSON stays valid."""
+    import json
+    import torch
+    from byzantine_consensus_llm_agents_amd.bcg import prompts as P
+    from byzantine_consensus_llm_agents_amd.engine import GuidedDecodingParams, LLM, SamplingParams
+    llm = LLM("bcg/tiny-qwen3", backend="torch", seed=3, max_model_len=512, kv_cache_gb=0.02,
+              max_batch_seqs=8, budget_aware_json=True, kv_cache_dtype="fp8")
+    assert llm.backend.k_cache.dtype == torch.float8_e4m3fn
+    params = [SamplingParams(temperature=0.5, max_tokens=40,
+                             guided_decoding=GuidedDecodingParams(json=P.honest_decision_schema(0, 50)))] * 3
+    outs = llm.generate([f"<|im_start|>user\nagent_{i}<|im_end|>\n<|im_start|>assistant\n" for i in range(3)],
+                        params)
+    for o in outs:
+        assert "value" in json.loads(o.outputs[0].text)
+    assert llm.backend.k_cache.float().abs().sum() > 0
+    llm.shutdown()

@@ -36,16 +36,20 @@ def test_silu_mul(hip):
     _close(hip.silu_mul(gu), R.silu_mul(gu), atol=2e-2)
 
 
-def _caches(L, NB, n_kv, hd, BS=16, fill=True):
+def _caches(L, NB, n_kv, hd, BS=16, fill=True, dtype=torch.bfloat16):
     k = torch.randn(L, NB, n_kv, BS, hd, device="cuda", dtype=torch.bfloat16) if fill else \
         torch.zeros(L, NB, n_kv, BS, hd, device="cuda", dtype=torch.bfloat16)
     v = torch.randn(L, NB, n_kv, hd, BS, device="cuda", dtype=torch.bfloat16) if fill else \
         torch.zeros(L, NB, n_kv, hd, BS, device="cuda", dtype=torch.bfloat16)
-    return k, v
+    return k.to(dtype), v.to(dtype)
 
 
+F8 = torch.float8_e4m3fn
+
+
+@pytest.mark.parametrize("kv_dtype", [torch.bfloat16, F8])
 @pytest.mark.parametrize("n_q,n_kv,hd,qk_norm", [(40, 8, 128, True), (14, 2, 64, False), (48, 8, 128, False)])
-def test_qk_norm_rope_kv_write(hip, n_q, n_kv, hd, qk_norm):
+def test_qk_norm_rope_kv_write(hip, n_q, n_kv, hd, qk_norm, kv_dtype):
     torch.manual_seed(1)
     T, L, NB = 29, 2, 12
     qkv = torch.randn(T, (n_q + 2 * n_kv) * hd, device="cuda", dtype=torch.bfloat16)
@@ -54,13 +58,20 @@ def test_qk_norm_rope_kv_write(hip, n_q, n_kv, hd, qk_norm):
     qn = (torch.rand(hd, device="cuda") + 0.5).to(torch.bfloat16) if qk_norm else None
     kn = (torch.rand(hd, device="cuda") + 0.5).to(torch.bfloat16) if qk_norm else None
     cs = R.rope_cache(8192, hd, 1e6, "cuda")
-    k1, v1 = _caches(L, NB, n_kv, hd, fill=False)
-    k2, v2 = _caches(L, NB, n_kv, hd, fill=False)
+    if kv_dtype == F8:
+        qkv[:3, :8] = torch.tensor([600.0, -1e4, 1e-4, 447.0, 0.01, -0.3, 3.0, 12.5], dtype=torch.bfloat16)
+    k1, v1 = _caches(L, NB, n_kv, hd, fill=False, dtype=kv_dtype)
+    k2, v2 = _caches(L, NB, n_kv, hd, fill=False, dtype=kv_dtype)
     q_ref = R.qk_norm_rope_kv_write(qkv, pos, slots, n_q, n_kv, hd, qn, kn, 1e-6, cs, k1, v1, 1)
     q = hip.qk_norm_rope_kv_write(qkv, pos, slots, n_q, n_kv, hd, qn, kn, 1e-6, cs, k2, v2, 1)
     _close(q, q_ref, atol=3e-2)
-    _close(k2, k1, atol=3e-2)
-    _close(v2, v1, atol=0, rtol=0)
+    if kv_dtype == F8:  # e4m3: 3 mantissa bits; a one-ulp rounding difference is 6.25 %
+        assert torch.isfinite(k2.float()).all() and torch.isfinite(v2.float()).all()
+        _close(k2, k1, atol=3e-2, rtol=0.07)
+        assert torch.equal(v2.view(torch.uint8), v1.view(torch.uint8))  # V: same bf16 -> fp8 rounding
+    else:
+        _close(k2, k1, atol=3e-2)
+        _close(v2, v1, atol=0, rtol=0)
 
 
 def _tables(B, lens, NB, max_blocks, gen):
@@ -74,12 +85,13 @@ def _tables(B, lens, NB, max_blocks, gen):
     return tables.cuda()
 
 
+@pytest.mark.parametrize("kv_dtype", [torch.bfloat16, F8])
 @pytest.mark.parametrize("n_q,n_kv,hd", [(40, 8, 128), (16, 2, 128), (14, 2, 64)])
-def test_paged_attention_decode(hip, n_q, n_kv, hd):
+def test_paged_attention_decode(hip, n_q, n_kv, hd, kv_dtype):
     gen = torch.Generator().manual_seed(2)
     lens = [1, 15, 16, 17, 255, 256, 257, 700, 1500]
     B, NB, L = len(lens), 256, 2
-    k, v = _caches(L, NB, n_kv, hd)
+    k, v = _caches(L, NB, n_kv, hd, dtype=kv_dtype)
     tables = _tables(B, lens, NB, 128, gen)
     seq = torch.tensor(lens, dtype=torch.int32, device="cuda")
     q = torch.randn(B, n_q, hd, device="cuda", dtype=torch.bfloat16)
@@ -97,15 +109,15 @@ def _prefill_tiles(q_start, seq_lens):
     return torch.tensor(tiles, dtype=torch.int32, device="cuda")
 
 
-@pytest.mark.parametrize("nt", [1, 2, 4])
+@pytest.mark.parametrize("nt,kv_dtype", [(1, torch.bfloat16), (2, torch.bfloat16), (4, torch.bfloat16), (4, F8)])
 @pytest.mark.parametrize("n_q,n_kv,hd", [(40, 8, 128), (14, 2, 64), (48, 8, 128)])
-def test_paged_attention_prefill(hip, n_q, n_kv, hd, nt):
+def test_paged_attention_prefill(hip, n_q, n_kv, hd, nt, kv_dtype):
     gen = torch.Generator().manual_seed(3)
     # (cached prefix, new tokens)
     spec = [(0, 1), (0, 37), (16, 50), (32, 64), (0, 300), (160, 129)]
     ctx = [a + b for a, b in spec]
     B, NB, L = len(spec), 256, 1
-    k, v = _caches(L, NB, n_kv, hd)
+    k, v = _caches(L, NB, n_kv, hd, dtype=kv_dtype)
     tables = _tables(B, ctx, NB, 64, gen)
     q_start = [0]
     for _, n in spec:
