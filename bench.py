@@ -143,6 +143,9 @@ def _heartbeat(llm, stop: threading.Event, every: float = 30.0):
 
 def main():
     args = parse()
+    # stdout carries exactly ONE line (the JSON result): anything else -- e.g. the
+    # reference's console messages when an agent fails all JSON retries -- goes to stderr
+    result_out, sys.stdout = sys.stdout, sys.stderr
     if os.environ.get("BCG_STACKS_AFTER"):  # debugging aid: dump every thread's stack periodically
         import faulthandler
         faulthandler.dump_traceback_later(float(os.environ["BCG_STACKS_AFTER"]), repeat=True, file=sys.stderr)
@@ -251,7 +254,7 @@ def main():
                        "outcomes_rank0": pool.outcomes,
                        "phases_rank0": llm.backend.timer.summary() if hasattr(llm.backend, "timer") else {}},
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=result_out, flush=True)
     stop_hb.set()
     llm.shutdown()
     if world > 1:

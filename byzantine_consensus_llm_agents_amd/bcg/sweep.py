@@ -29,6 +29,7 @@ import json
 import os
 import queue
 import random
+import sys
 import threading
 import time
 from typing import Dict, List
@@ -168,6 +169,14 @@ def summarize(games: List[Dict], elapsed: float, n_gpus: int) -> Dict:
 
 def main(argv=None) -> Dict:
     args = build_parser().parse_args(argv)
+    saved_stdout, sys.stdout = sys.stdout, sys.stderr  # agents' console messages; the summary line stays alone
+    try:
+        return _main(args)
+    finally:
+        sys.stdout = saved_stdout
+
+
+def _main(args) -> Dict:
     from ..parallel.groups import destroy, env_layout, init_distributed
     from . import config as C
     from .engine_agent import EngineAgent
@@ -258,7 +267,7 @@ def main(argv=None) -> Dict:
         with open(args.out, "w") as fh:
             json.dump(summary, fh, indent=2)
         brief = {k: v for k, v in summary.items() if k != "per_game"}
-        print(json.dumps(brief), flush=True)
+        print(json.dumps(brief), file=sys.__stdout__ if sys.stdout is sys.stderr else sys.stdout, flush=True)
     llm.shutdown()
     EngineAgent._shared_llm = None
     destroy()
