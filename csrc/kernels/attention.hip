@@ -52,6 +52,7 @@ __device__ __forceinline__ size_t block_base(const KVGeom& g, int blk, int kvh) 
 // the raw 8 e4m3fn bytes, widened to bf16 only right before their MFMA so the
 // loads of the next chunk stay in flight (converting at load time would wait).
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 template <int HD, bool F8 = false>
 struct Chunk {
@@ -155,7 +156,6 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16
 #pragma unroll
     for (int dt = 0; dt < HD / 16; ++dt) {
       o[dt] *= alpha;
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
       u32x4 va = __builtin_bit_cast(u32x4, to_bf16x8(c.v[dt]));
 #pragma unroll
       for (int j2 = 0; j2 < 4; ++j2) va[j2] &= keep[j2];
@@ -453,6 +453,181 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   }
 }
 
+// ---- prefill, LDS-shared K/V (bf16 caches, HD = 128) ------------------------
+// A workgroup = one 64-row tile x one kv head x GT of its query heads.  Each
+// 32-token K/V chunk (16 KiB) is loaded ONCE per workgroup -- 4 x 16 B per
+// thread, coalesced 4 KiB block runs -- into a double-buffered, XOR-swizzled
+// LDS image, and all 4 waves (16 rows each) x GT heads read their MFMA
+// operands from it: every global K/V byte feeds 4*GT times the MFMAs of the
+// register-direct kernel above.  Pipeline per chunk: issue the next chunk's
+// global loads -> compute this chunk from LDS -> write the staged registers to
+// the other buffer -> barrier.
+//   K image: row = token (256 B); 16-B column j stored at j ^ swz(t),
+//            swz(t) = (t ^ (t >> 4)) & 15: the 16 rows one MFMA fragment
+//            gathers land on 16 different bank groups.
+//   V image: row = dim d (64 B = 32 tokens); 16-B column h stored at
+//            h ^ ((d >> 2) & 3): 16 consecutive rows -> 16 bank groups.
+constexpr int LDS_K_BYTES = CHUNK * 128 * 2;   // 8 KiB
+constexpr int LDS_V_BYTES = 128 * CHUNK * 2;   // 8 KiB
+
+__device__ __forceinline__ int k_swz(int t) { return (t ^ (t >> 4)) & 15; }
+
+template <int GT>
+__global__ __launch_bounds__(256) void prefill_attn_lds_kernel(
+    const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
+    const int* __restrict__ q_start, const int* __restrict__ seq_lens, const int* __restrict__ tiles,
+    int n_q, float scale_log2, bf16_t* __restrict__ out) {
+  constexpr int HD = 128;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2][LDS_K_BYTES + LDS_V_BYTES];
+  const int tile = blockIdx.x, kvh = blockIdx.y;
+  const int G = n_q / g.n_kv;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 15, h = lane >> 4;
+  const int b = tiles[3 * tile], q_begin = tiles[3 * tile + 1], q_end = tiles[3 * tile + 2];
+  const int ctx = seq_lens[b];
+  const int qs = q_start[b], qlen = q_start[b + 1] - qs;
+  const int pos0 = ctx - qlen;
+  const int* table = block_tables + static_cast<size_t>(b) * max_blocks;
+  const int kv_end = pos0 + (q_end - 1 - qs) + 1;  // keys visible to the tile's last row
+  const int nchunk = (kv_end + CHUNK - 1) / CHUNK;
+  const int nblk = (kv_end + BS - 1) / BS;
+
+  // this wave's 16 rows x GT heads
+  const int row0 = q_begin + 16 * w;
+  const bool wave_rows = row0 < q_end;  // wave-uniform; idle waves still stage K/V and hit barriers
+  const int my_row = row0 + r;
+  const bool row_ok = my_row < q_end;
+  const int my_pos = pos0 + (my_row - qs);
+  const int first_pos = pos0 + (row0 - qs);
+  const int w_end = wave_rows ? pos0 + (min(row0 + 15, q_end - 1) - qs) + 1 : 0;
+  bf16x8 bq[GT][HD / 32];
+  float m[GT], l[GT];
+  f32x4 o[GT][HD / 16];
+#pragma unroll
+  for (int gt = 0; gt < GT; ++gt) {
+    const int qh = kvh * G + blockIdx.z * GT + gt;
+    load_q<HD>(bq[gt], q + (static_cast<size_t>(row_ok ? my_row : (wave_rows ? row0 : q_begin)) * n_q + qh) * HD,
+               row_ok, lane);
+    m[gt] = -INFINITY;
+    l[gt] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) o[gt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // staging: thread tid moves 16-B piece p = tid + 256*i (i < 4) of the chunk:
+  // i = 0,1 -> K (piece = blk_local*256 + token*16 + j), i = 2,3 -> V (blk_local*256 + d*2 + half)
+  u32x4 stage[4];
+  auto issue = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int piece = tid + 256 * (i & 1);
+      const int bl = piece >> 8, within = piece & 255;
+      const int blk = table[min(2 * c + bl, nblk - 1)];
+      const size_t base = block_base<HD>(g, blk, kvh);
+      const bf16_t* src = (i < 2 ? g.k : g.v) + base + within * 8;
+      stage[i] = *reinterpret_cast<const u32x4*>(src);
+    }
+  };
+  auto commit = [&](int buf) {
+    uint8_t* kimg = smem[buf];
+    uint8_t* vimg = smem[buf] + LDS_K_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int piece = tid + 256 * (i & 1);
+      const int bl = piece >> 8, within = piece & 255;
+      if (i < 2) {
+        const int t = bl * 16 + (within >> 4), j = within & 15;
+        *reinterpret_cast<u32x4*>(kimg + t * 256 + ((j ^ k_swz(t)) << 4)) = stage[i];
+      } else {
+        const int d = within >> 1, hh = bl * 2 + (within & 1);
+        *reinterpret_cast<u32x4*>(vimg + d * 64 + ((hh ^ ((d >> 2) & 3)) << 4)) = stage[i];
+      }
+    }
+  };
+
+  issue(0);
+  commit(0);
+  __syncthreads();
+  for (int c = 0; c < nchunk; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nchunk) issue(c + 1);
+    if (wave_rows && c * CHUNK < w_end) {  // wave-uniform
+      const uint8_t* kimg = smem[buf];
+      const uint8_t* vimg = smem[buf] + LDS_K_BYTES;
+      Chunk<HD> ch;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int t = 8 * (r >> 2) + 4 * u + (r & 3);
+#pragma unroll
+        for (int kk = 0; kk < HD / 32; ++kk)
+          ch.k[u][kk] = *reinterpret_cast<const bf16x8*>(kimg + t * 256 + (((kk * 4 + h) ^ k_swz(t)) << 4));
+      }
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) {
+        const int d = dt * 16 + r;
+        ch.v[dt] = *reinterpret_cast<const bf16x8*>(vimg + d * 64 + ((h ^ ((d >> 2) & 3)) << 4));
+      }
+      if ((c + 1) * CHUNK <= first_pos) {  // every key visible to every row of this wave
+#pragma unroll
+        for (int gt = 0; gt < GT; ++gt)
+          compute_chunk<HD, Causal, false>(ch, bq[gt], c * CHUNK, w_end, Causal{my_pos}, scale_log2, m[gt],
+                                           l[gt], o[gt], lane);
+      } else {
+#pragma unroll
+        for (int gt = 0; gt < GT; ++gt)
+          compute_chunk<HD, Causal, true>(ch, bq[gt], c * CHUNK, w_end, Causal{my_pos}, scale_log2, m[gt],
+                                          l[gt], o[gt], lane);
+      }
+    }
+    if (c + 1 < nchunk) commit(buf ^ 1);
+    __syncthreads();
+  }
+  if (!row_ok) return;
+#pragma unroll
+  for (int gt = 0; gt < GT; ++gt) {
+    const int qh = kvh * G + blockIdx.z * GT + gt;
+    const float inv = l[gt] > 0.f ? 1.f / l[gt] : 0.f;
+    bf16_t* orow = out + (static_cast<size_t>(my_row) * n_q + qh) * HD;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) {
+      u16x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = f2bf(o[gt][dt][i] * inv);
+      *reinterpret_cast<u16x4*>(orow + dt * 16 + 4 * h) = v;
+    }
+  }
+}
+
+// heads per workgroup for the LDS kernel: the largest divisor of G that is <= 5
+inline int lds_group_tile(int G) {
+  for (int gt = 5; gt >= 1; --gt)
+    if (G % gt == 0) return gt;
+  return 1;
+}
+
+int launch_prefill_lds(int n_tiles, int n_q, int n_kv, const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
+                       const int* q_start, const int* seq_lens, const int* tiles, float sl, bf16_t* out,
+                       hipStream_t stream) {
+  const int G = n_q / n_kv, gt = lds_group_tile(G);
+  const dim3 grid(n_tiles, n_kv, G / gt);
+  switch (gt) {
+#define BCG_LDS_CASE(GT)                                                                                         \
+  case GT:                                                                                                       \
+    hipLaunchKernelGGL(prefill_attn_lds_kernel<GT>, grid, dim3(256), 0, stream, q, g, tables, max_blocks,      \
+                       q_start, seq_lens, tiles, n_q, sl, out);                                                  \
+    break;
+    BCG_LDS_CASE(1)
+    BCG_LDS_CASE(2)
+    BCG_LDS_CASE(3)
+    BCG_LDS_CASE(4)
+    BCG_LDS_CASE(5)
+#undef BCG_LDS_CASE
+    default:
+      return -2;
+  }
+  return 0;
+}
+
 template <int HD, bool F8>
 int launch_prefill(int nt, int n_tiles, int n_q, const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
                    const int* q_start, const int* seq_lens, const int* tiles, float sl, bf16_t* out,
@@ -532,7 +707,8 @@ BCG_API int bcg_paged_attention_decode_exp(const void* q, const void* k_cache, c
   return BCG_CHECK_LAUNCH();
 }
 
-// nt: query tiles of 16 rows per wave (1, 2 or 4) -- see prefill_attn_kernel.
+// nt: query tiles of 16 rows per wave (1, 2 or 4) -- see prefill_attn_kernel; 0 = the LDS-shared
+// K/V kernel (bf16 caches, head_dim 128; other shapes fall back to nt = 4).
 BCG_API int bcg_paged_attention_prefill(const void* q, const void* k_cache, const void* v_cache, int layer,
                                         int num_blocks, int n_kv, const int* block_tables, int max_blocks,
                                         const int* q_start, const int* seq_lens, const int* tiles, int n_tiles,
@@ -544,7 +720,11 @@ BCG_API int bcg_paged_attention_prefill(const void* q, const void* k_cache, cons
   const bf16_t* qb = static_cast<const bf16_t*>(q);
   bf16_t* ob = static_cast<bf16_t*>(out);
   int rc;
-  if (hd == 128)
+  if (nt == 0 && !(hd == 128 && !kv_fp8)) nt = 4;
+  if (nt == 0)  // LDS-shared K/V variant
+    rc = launch_prefill_lds(n_tiles, n_q, n_kv, qb, g, block_tables, max_blocks, q_start, seq_lens, tiles, sl, ob,
+                            stream);
+  else if (hd == 128)
     rc = kv_fp8 ? launch_prefill<128, true>(nt, n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens,
                                             tiles, sl, ob, stream)
                 : launch_prefill<128, false>(nt, n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens,

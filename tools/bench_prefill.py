@@ -88,6 +88,7 @@ def main():
     ap.add_argument("--m", default="16384")
     ap.add_argument("--modes", default="default,tuned,rocblas")
     ap.add_argument("--skip-gemm", action="store_true")
+    ap.add_argument("--attn-model", default=None, help="model geometry for the attention runs")
     args = ap.parse_args()
     cfg = get_model_config(args.model)
     out = {"model": cfg.name, "gemm": {}, "attention": []}
@@ -108,9 +109,10 @@ def main():
             out["gemm"][f"{mode}_M{M}"] = gemms(cfg, M, mode)
         torch.backends.cuda.preferred_blas_library("cublaslt")
         torch.cuda.tunable.enable(False)
-    for nt in (1, 2, 4):
+    acfg = get_model_config(args.attn_model) if args.attn_model else cfg
+    for nt in (0, 4):
         for n, p, pre in ((12, 1024, 512), (16, 900, 400), (8, 2048, 0)):
-            out["attention"].append(attention(cfg, n, p, pre, nt))
+            out["attention"].append(attention(acfg, n, p, pre, nt))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "bench_prefill.json"), "w") as fh:
         json.dump(out, fh, indent=1)
