@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--model", default="qwen3-14b")
     ap.add_argument("--honest", type=int, default=8)
     ap.add_argument("--byzantine", type=int, default=2)
-    ap.add_argument("--sims-per-gpu", type=int, default=96)
+    ap.add_argument("--sims-per-gpu", type=int, default=128)
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--max-rounds", type=int, default=50)
     ap.add_argument("--seed", type=int, default=1234)
