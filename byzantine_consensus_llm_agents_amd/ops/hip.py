@@ -202,7 +202,7 @@ def hip_ops() -> SimpleNamespace:
         _check(lib.bcg_paged_attention_prefill(
             _p(q), _p(k_cache), _p(v_cache), layer, NB, n_kv, _p(block_tables), block_tables.shape[1],
             _p(q_start), _p(seq_lens), _p(tiles), tiles.shape[0], n_q, hd, BS, scale, _p(out),
-            nt or prefill_nt, _kv_fp8(k_cache, v_cache), _stream()), "paged_attention_prefill")
+            prefill_nt if nt is None else nt, _kv_fp8(k_cache, v_cache), _stream()), "paged_attention_prefill")
         return out
 
     use_skinny = os.environ.get("BCG_SKINNY_GEMM", "0") == "1"  # hipBLASLt wins (bench_ops r1)
