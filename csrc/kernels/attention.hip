@@ -98,6 +98,25 @@ __device__ __forceinline__ void load_chunk(Chunk<HD, F8>& c, const KVGeom& g, in
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// Reductions over the 4 lane rows (h = lane >> 4) that share a query column:
+// v_permlane16_swap (rows 0<->1, 2<->3) then v_permlane32_swap (0<->2, 1<->3),
+// two VALU ops each instead of ds_bpermute round trips through the LDS
+// crossbar (~100 cycles apiece, four of them in series per chunk).  Both
+// halves of each swap are combined, so every lane gets identical bits.
+__device__ __forceinline__ float rows_max(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+__device__ __forceinline__ float rows_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 // Online-softmax update + O^T accumulation for one chunk starting at token t0.
 // visible(t) decides masking (t = absolute token index); kv_end bounds V reads.
 // MASKED = false: the caller guarantees every token of the chunk is visible to
@@ -125,8 +144,7 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16
     p[j] = (!MASKED || (t < kv_end && visible(t))) ? sv * scale_log2 : -INFINITY;
     mx = fmaxf(mx, p[j]);
   }
-  mx = fmaxf(mx, __shfl_xor(mx, 16, WAVE));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, WAVE));
+  mx = rows_max(mx);
   // no early exit: the MFMAs below must run with every lane active
   const float m_new = fmaxf(m, mx);
   const float m_use = m_new == -INFINITY ? 0.f : m_new;
@@ -137,8 +155,7 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16
     p[j] = exp2f(p[j] - m_use);
     ps += p[j];
   }
-  ps += __shfl_xor(ps, 16, WAVE);
-  ps += __shfl_xor(ps, 32, WAVE);
+  ps = rows_sum(ps);
   l = l * alpha + ps;
   m = m_new;
   bf16x8 bp;
