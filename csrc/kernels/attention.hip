@@ -36,6 +36,7 @@ constexpr int BS = 16;            // KV block size (tokens)
 constexpr int DEC_WAVES = 4;
 constexpr int CHUNK = 32;
 constexpr float LOG2E = 1.4426950408889634f;
+constexpr float RESCALE_LOG2 = 8.f;  // lazy online-softmax rescale threshold (log2 units)
 
 struct KVGeom {
   const bf16_t* k;   // [L, NB, n_kv, BS, HD]
@@ -145,10 +146,20 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16
     mx = fmaxf(mx, p[j]);
   }
   mx = rows_max(mx);
-  // no early exit: the MFMAs below must run with every lane active
-  const float m_new = fmaxf(m, mx);
-  const float m_use = m_new == -INFINITY ? 0.f : m_new;
-  const float alpha = m == -INFINITY ? 0.f : exp2f(m - m_use);
+  // Lazy rescale: the reference max m only moves when some column's chunk max
+  // exceeds it by more than 2^RESCALE_LOG2 (then P <= 2^8 stays exact in fp32 /
+  // bf16 and l cannot overflow over an 8k context).  Rescaling O is 32 VALU
+  // multiplies plus the accumulator moves around them -- the kernels were
+  // VALU-bound on it (14 VALU per MFMA, PMC); after the first chunks it is rare.
+  if (__builtin_amdgcn_ballot_w64(mx > m + RESCALE_LOG2) != 0) {  // wave-uniform
+    const float m_new = fmaxf(m, mx);
+    const float alpha = m == -INFINITY ? 0.f : exp2f(m - m_new);
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) o[dt] *= alpha;
+    m = m_new;
+  }
+  const float m_use = m == -INFINITY ? 0.f : m;
   float ps = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -156,8 +167,7 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16
     ps += p[j];
   }
   ps = rows_sum(ps);
-  l = l * alpha + ps;
-  m = m_new;
+  l += ps;
   bf16x8 bp;
 #pragma unroll
   for (int j = 0; j < 8; ++j) bp[j] = static_cast<__bf16>(p[j]);
@@ -172,7 +182,6 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16
     }
 #pragma unroll
     for (int dt = 0; dt < HD / 16; ++dt) {
-      o[dt] *= alpha;
       u32x4 va = __builtin_bit_cast(u32x4, to_bf16x8(c.v[dt]));
 #pragma unroll
       for (int j2 = 0; j2 < 4; ++j2) va[j2] &= keep[j2];
@@ -180,10 +189,8 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16
     }
   } else {
 #pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt) {
-      o[dt] *= alpha;
+    for (int dt = 0; dt < HD / 16; ++dt)
       o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(to_bf16x8(c.v[dt]), bp, o[dt], 0, 0, 0);
-    }
   }
 }
 
