@@ -123,7 +123,7 @@ __device__ __forceinline__ float rows_sum(float v) {
 // MASKED = false: the caller guarantees every token of the chunk is visible to
 // every column (wave-uniform), so the per-token mask and the V-tail zeroing
 // (~60 VALU ops per chunk beside 16 MFMAs) are skipped.
-template <int HD, typename Vis, bool MASKED = true, bool F8 = false>
+template <int HD, typename Vis, bool MASKED = true, bool F8 = false, bool LAZY = true>
 __device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16x8 (&bq)[HD / 32], int t0, int kv_end,
                                               Vis visible, float scale_log2, float& m, float& l,
                                               f32x4 (&o)[HD / 16], int lane) {
@@ -151,12 +151,23 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16
   // bf16 and l cannot overflow over an 8k context).  Rescaling O is 32 VALU
   // multiplies plus the accumulator moves around them -- the kernels were
   // VALU-bound on it (14 VALU per MFMA, PMC); after the first chunks it is rare.
-  if (__builtin_amdgcn_ballot_w64(mx > m + RESCALE_LOG2) != 0) {  // wave-uniform
-    const float m_new = fmaxf(m, mx);
-    const float alpha = m == -INFINITY ? 0.f : exp2f(m - m_new);
-    l *= alpha;
+  if constexpr (LAZY) {
+    if (__builtin_amdgcn_ballot_w64(mx > m + RESCALE_LOG2) != 0) {  // wave-uniform
+      const float m_new = fmaxf(m, mx);
+      const float alpha = m == -INFINITY ? 0.f : exp2f(m - m_new);
+      l *= alpha;
 #pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt) o[dt] *= alpha;
+      for (int dt = 0; dt < HD / 16; ++dt) o[dt] *= alpha;
+      m = m_new;
+    }
+  }
+  // eager (LAZY = false): rescale every chunk, O folded into the P.V loop below --
+  // the branch-free form keeps fewer registers live (no spills at NT = 4)
+  float alpha = 1.f;
+  if constexpr (!LAZY) {
+    const float m_new = fmaxf(m, mx);
+    alpha = m == -INFINITY ? 0.f : exp2f(m - (m_new == -INFINITY ? 0.f : m_new));
+    l *= alpha;
     m = m_new;
   }
   const float m_use = m == -INFINITY ? 0.f : m;
@@ -182,6 +193,7 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16
     }
 #pragma unroll
     for (int dt = 0; dt < HD / 16; ++dt) {
+      if constexpr (!LAZY) o[dt] *= alpha;
       u32x4 va = __builtin_bit_cast(u32x4, to_bf16x8(c.v[dt]));
 #pragma unroll
       for (int j2 = 0; j2 < 4; ++j2) va[j2] &= keep[j2];
@@ -189,8 +201,10 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16
     }
   } else {
 #pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt)
+    for (int dt = 0; dt < HD / 16; ++dt) {
+      if constexpr (!LAZY) o[dt] *= alpha;
       o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(to_bf16x8(c.v[dt]), bp, o[dt], 0, 0, 0);
+    }
   }
 }
 
@@ -452,11 +466,11 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
     for (int nt = 0; nt < NT; ++nt) {
       if (c * CHUNK >= sub_end[nt]) continue;  // wave-uniform: chunk wholly in this sub-tile's causal future
       if ((c + 1) * CHUNK <= sub_first[nt])     // wave-uniform: every key visible to every row
-        compute_chunk<HD, Causal, false, F8>(cur, bq[nt], c * CHUNK, sub_end[nt], Causal{my_pos[nt]},
-                                             scale_log2, m[nt], l[nt], o[nt], lane);
+        compute_chunk<HD, Causal, false, F8, false>(cur, bq[nt], c * CHUNK, sub_end[nt], Causal{my_pos[nt]},
+                                                    scale_log2, m[nt], l[nt], o[nt], lane);
       else
-        compute_chunk<HD, Causal, true, F8>(cur, bq[nt], c * CHUNK, sub_end[nt], Causal{my_pos[nt]},
-                                            scale_log2, m[nt], l[nt], o[nt], lane);
+        compute_chunk<HD, Causal, true, F8, false>(cur, bq[nt], c * CHUNK, sub_end[nt], Causal{my_pos[nt]},
+                                                   scale_log2, m[nt], l[nt], o[nt], lane);
     }
     cur = nxt;
   }
