@@ -68,6 +68,11 @@ class EngineArgs:
     overlap_prefill: bool = False  # prefill on its own HIP stream, concurrent with decode bursts
     precapture_graphs: bool = True  # capture every decode bucket at the first burst (and after FSM growth)
     kv_cache_dtype: str = "auto"    # "auto" = activation dtype (bf16); "fp8" = OCP e4m3fn (half the KV bytes)
+    # admission batching (0 = admit at once): queue prompts for up to this many decode
+    # bursts while >= admit_min_live rows decode, until >= frac x prefill_chunk_tokens wait
+    admit_max_wait: int = 0
+    admit_min_live: int = 64
+    admit_min_tokens_frac: float = 1.5
 
     @classmethod
     def from_configs(cls, model: str, backend: str, weights: Optional[str] = None,
@@ -89,7 +94,8 @@ class EngineArgs:
                    honor_max_num_seqs=ec.get("honor_max_num_seqs", False),
                    overlap_prefill=ec.get("overlap_prefill", False),
                    precapture_graphs=ec.get("precapture_graphs", True),
-                   kv_cache_dtype=ec.get("kv_cache_dtype", "auto"))
+                   kv_cache_dtype=ec.get("kv_cache_dtype", "auto"),
+                   admit_max_wait=int(ec.get("admit_max_wait", 0)))
         dtype = ec.get("dtype", "bfloat16")
         args.dtype = getattr(torch, dtype) if isinstance(dtype, str) else dtype
         for key, value in kw.items():
@@ -167,6 +173,7 @@ class InferenceEngine:
         self.overlap = bool(args.overlap_prefill and self.device.type == "cuda" and self.tp.size == 1)
         self.prefill_stream = torch.cuda.Stream(self.device) if self.overlap else None
         self._inflight = None
+        self._bursts = 0         # decode bursts launched (admission-batching clock)
         self._snap = None        # host copy of (done, gen_count, out_tokens) after the last burst
         self._engine_errors = 0
         self._snap_buf = None
@@ -306,7 +313,7 @@ class InferenceEngine:
             with self.timer.phase("fsm_compile"):
                 base = self.fsm.get(schema) if schema is not None else -1
             seq = _Seq(0, p_ids, max(1, int(p.max_tokens)), float(p.temperature), base)
-            req = _Request(seq)
+            req = _Request(seq, self._bursts)
             if len(p_ids) == 0 or len(p_ids) + seq.max_new > self.args.max_model_len or seq.max_new > OUT_WIDTH:
                 req.finish("")  # reference behaviour: the caller sees an unparsable (empty) output
             reqs.append(req)
@@ -423,9 +430,27 @@ class InferenceEngine:
         """Rows the decode graphs advance (prefill done)."""
         return [i for i, r in enumerate(self.slots) if r is not None and not r.pending]
 
+    def _admission_deferred(self) -> bool:
+        """Admission batching: while the decode batch is well fed, let prompts queue up
+        to a full prefill chunk (the prefill GEMMs run at their tuned M instead of
+        ragged 2-8k-token tails) -- bounded by `admit_max_wait` bursts of waiting.
+        Deterministic under TP: it depends on queue contents and burst counts only."""
+        a = self.args
+        if a.admit_max_wait <= 0:
+            return False
+        live = sum(1 for r in self.slots if r is not None and not r.pending)
+        if live < a.admit_min_live:
+            return False
+        if self._bursts - self._waiting[0].enq_burst >= a.admit_max_wait:
+            return False
+        queued = sum(len(r.seq.prompt_ids) for r in self._waiting)
+        return queued < a.admit_min_tokens_frac * a.prefill_chunk_tokens
+
     def _admit(self):
         with self._cv:
             if not self._waiting:
+                return
+            if self._admission_deferred():
                 return
             free = [i for i, r in enumerate(self.slots) if r is None]
             cap = self.args.max_batch_seqs
@@ -510,6 +535,7 @@ class InferenceEngine:
         with self.timer.phase("decode"):
             steps = self.graphs.run_burst(n) if self.graphs is not None else self._eager_burst(n)
         self.stats["decode_steps"] += steps
+        self._bursts += 1
 
     def _eager_burst(self, n: int) -> int:
         view = {k: v[:n] for k, v in self.state.items()}
@@ -704,10 +730,11 @@ class InferenceEngine:
 
 
 class _Request:
-    __slots__ = ("seq", "row", "text", "exc", "event", "pending")
+    __slots__ = ("seq", "row", "text", "exc", "event", "pending", "enq_burst")
 
-    def __init__(self, seq: _Seq):
+    def __init__(self, seq: _Seq, enq_burst: int = 0):
         self.seq, self.row, self.text, self.exc, self.pending = seq, -1, "", None, False
+        self.enq_burst = enq_burst
         self.event = threading.Event()
 
     def finish(self, text: str):

@@ -116,3 +116,38 @@ def test_engine_fp8_kv_cache_cpu(fresh_engine_state):
         assert "value" in json.loads(o.outputs[0].text)
     assert llm.backend.k_cache.float().abs().sum() > 0
     llm.shutdown()
+
+
+def test_engine_admission_batching_cpu(fresh_engine_state):
+    """Deferred admission (prompts queue while others decode) still completes every request."""
+    import json
+    import threading
+    from byzantine_consensus_llm_agents_amd.bcg import prompts as P
+    from byzantine_consensus_llm_agents_amd.engine import GuidedDecodingParams, LLM, SamplingParams
+    llm = LLM("bcg/tiny-qwen3", backend="torch", seed=4, max_model_len=512, kv_cache_gb=0.05,
+              max_batch_seqs=16, budget_aware_json=True, admit_max_wait=3, admit_min_live=1,
+              prefill_chunk_tokens=4096)
+    assert llm.backend.args.admit_max_wait == 3
+    llm.start_continuous_batching()
+    schema = P.vote_schema(P.HONEST_VOTE_OPTIONS)
+    results, errors = [], []
+
+    def client(k):
+        try:
+            for rnd in range(2):
+                params = [SamplingParams(temperature=0.5, max_tokens=12 + 4 * k,
+                                         guided_decoding=GuidedDecodingParams(json=schema))] * 2
+                outs = llm.generate([f"<|im_start|>user\nc{k} r{rnd} {j}<|im_end|>\n<|im_start|>assistant\n"
+                                     for j in range(2)], params)
+                results.extend(json.loads(o.outputs[0].text)["decision"] for o in outs)
+        except BaseException as exc:
+            errors.append(exc)
+
+    threads = [threading.Thread(target=client, args=(k,)) for k in range(4)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=300)
+    llm.shutdown()
+    assert not errors, errors[0]
+    assert len(results) == 16 and set(results) <= {"stop", "continue"}
