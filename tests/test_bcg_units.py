@@ -1,4 +1,5 @@
 """Unit tests of the simulation layer (rules from SURVEY.md §2.4)."""
+import os
 import random
 
 import pytest
@@ -94,3 +95,20 @@ def test_deadline():
         g.advance_round({"agent_0": False, "agent_1": False})
     assert g.game_over and g.current_round == 4 and g.termination_reason == "max_rounds"
     assert g.get_statistics()["consensus_outcome"] == "timeout"
+
+
+def test_reference_layout_shims_run_both_ways(tmp_path):
+    """`cd byzantine_consensus_game; python main.py` (the reference workflow) and `python -m ...main`."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    args = ["--honest", "3", "--byzantine", "1", "--rounds", "2", "--engine", "fake", "--seed", "2"]
+    env = dict(os.environ, PYTHONPATH=root)
+    a = subprocess.run([sys.executable, os.path.join(root, "byzantine_consensus_game", "main.py"), *args],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert a.returncode == 0, a.stderr
+    b = subprocess.run([sys.executable, "-m", "byzantine_consensus_game.main", *args], cwd=tmp_path, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert b.returncode == 0, b.stderr
+    assert os.path.exists(tmp_path / "results" / "json" / "run_001.json")
+    assert os.path.exists(tmp_path / "results" / "json" / "run_002.json")  # run numbers keep increasing
