@@ -88,6 +88,7 @@ def main():
     ap.add_argument("--m", default="16384")
     ap.add_argument("--modes", default="default,tuned,rocblas")
     ap.add_argument("--skip-gemm", action="store_true")
+    ap.add_argument("--skip-attn", action="store_true")
     ap.add_argument("--attn-model", default=None, help="model geometry for the attention runs")
     args = ap.parse_args()
     cfg = get_model_config(args.model)
@@ -110,7 +111,7 @@ def main():
         torch.backends.cuda.preferred_blas_library("cublaslt")
         torch.cuda.tunable.enable(False)
     acfg = get_model_config(args.attn_model) if args.attn_model else cfg
-    for nt in (0, 4):
+    for nt in (() if args.skip_attn else (0, 4)):
         for n, p, pre in ((12, 1024, 512), (16, 900, 400), (8, 2048, 0)):
             out["attention"].append(attention(acfg, n, p, pre, nt))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
