@@ -100,6 +100,11 @@ class FSMRegistry:
 
     def get(self, schema: Dict) -> int:
         key = self.key_of(schema)
+        # hit path without the lock: `_bases[key]` is published only after the rows are
+        # written, and a dict read is atomic, so callers no longer queue behind a compile
+        base = self._bases.get(key)
+        if base is not None:
+            return base
         with self._lock:
             base = self._bases.get(key)
             if base is not None:
