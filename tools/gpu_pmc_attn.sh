@@ -12,7 +12,7 @@ while read -r group; do
   timeout -s KILL 90 rocprofv3 --pmc $group --output-format csv -d gpurun_out/pmc_attn/p$i -o run -- \
     python tools/bench_prefill.py --skip-gemm > gpurun_out/pmc_attn/p$i.log 2>&1
   rc=$?
-  if [ $rc -ne 0 ]; then echo "pass $i failed rc=$rc: $group"; grep -i -m3 "error" gpurun_out/pmc_attn/p$i.log; [ $rc -eq 137 ] && exit 1; continue; fi
+  if [ $rc -ne 0 ]; then echo "pass $i failed rc=$rc: $group"; grep -i -m3 "error" gpurun_out/pmc_attn/p$i.log; exit 1; fi
   echo "pass $i ok: $group"
 done <<GROUPS
 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS
