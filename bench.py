@@ -2,52 +2,68 @@
 
 Metric (BASELINE.md "Measurement protocol"): accepted decide outputs +
 accepted vote outputs per wall-clock second, summed over every GPU of the
-node.  One "step" = one BCG round of every simulation running on the GPU (each
-round: all agents' decide prompts in one engine call, all vote prompts in one
-call, plus whatever retries the reference's retry ladder triggers).
+node.  Retries cost time but are not counted.
 
-Layout: one process per GPU (torchrun), data-parallel over independent
-simulation seeds (``--sims-per-gpu`` games share each GPU's engine, which
-serves them with continuous batching; a game that ends is replaced by a fresh
-seed so the pool stays full).  With ``--tp > 1`` groups of GPUs form
-tensor-parallel engines (RCCL all-reduce) fed by lock-step coalesced rounds.
+Unit of work.  ``--sims-per-gpu`` independent games (seeds) run continuously
+on each engine, each on its own thread; a game that ends is replaced by a
+fresh seed, so the continuously-batched decode stays full (steady state).  One
+"step" is one fixed wall-clock window of ``--window-s`` seconds of that pool;
+its decisions are the accepted decide/vote outputs completed inside it.  W
+warmup windows bring the pool to steady state (full batch, warm prefix cache,
+every decode graph captured), then K windows are timed between a barrier +
+``torch.cuda.synchronize()`` on both sides; the elapsed time is the max over
+ranks and the decision count the sum over DP replicas.  Nothing is skipped
+inside the timed region: every decision counted was fully generated,
+FSM-guided, parsed and validated by the game.
+
+Layout: one process per GPU.  ``--gpus N`` with no ``WORLD_SIZE`` in the
+environment launches N ranks itself (a ``torch.distributed.run`` child
+process, started before this process touches the GPU).  DP over seeds across
+engines; ``--tp > 1`` groups consecutive ranks into one tensor-parallel engine
+(rank 0 of the group schedules, the others execute its plans).
 
 Data: random-init weights of the real architecture and the synthetic
 byte-level BPE tokenizer (no network for checkpoints); the budget-aware JSON
-grammar guarantees schema-valid outputs from untrained weights, at the full
+grammar guarantees schema-valid outputs from untrained weights at the full
 max_tokens (300 decide / 200 vote) -- a pessimistic decode length.
 
-Timing: W warmup rounds, barrier + cuda.synchronize, K timed rounds,
-barrier + synchronize; the max time over ranks; rank 0 prints one JSON line.
+Deadline guard: if the run would pass ``--deadline-s`` (from process start),
+the timed loop stops early and the JSON line reports the windows actually
+timed (``steps``) -- the result line is always printed.
 """
 
 import argparse
 import json
 import os
 import random
+import socket
+import subprocess
 import sys
 import threading
 import time
 
+T_PROCESS0 = time.perf_counter()
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
 BASELINE_VALUE = None  # BASELINE.md: the reference publishes no number
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3, help="timed BCG rounds")
-    ap.add_argument("--warmup", type=int, default=1, help="untimed BCG rounds")
+    ap.add_argument("--steps", type=int, default=20, help="timed windows")
+    ap.add_argument("--warmup", type=int, default=5, help="untimed warmup windows")
+    ap.add_argument("--window-s", type=float, default=8.0, help="seconds per step (window)")
+    ap.add_argument("--deadline-s", type=float, default=540.0,
+                    help="stop timing early rather than run past this many seconds from process start")
     ap.add_argument("--model", default="qwen3-14b")
     ap.add_argument("--honest", type=int, default=8)
     ap.add_argument("--byzantine", type=int, default=2)
     ap.add_argument("--sims-per-gpu", type=int, default=128)
+    ap.add_argument("--ramp-s", type=float, default=None,
+                    help="start the games spread over this many seconds (default: half the warmup)")
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--max-rounds", type=int, default=50)
     ap.add_argument("--seed", type=int, default=1234)
@@ -62,100 +78,146 @@ def parse():
     ap.add_argument("--no-custom-allreduce", action="store_true",
                     help="TP collectives through RCCL only (no xGMI one-/two-shot kernels)")
     ap.add_argument("--verbose", action="store_true")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args) -> int:
+    """`--gpus N` without a launcher: run N ranks as a torchrun CHILD process.
+
+    Nothing here touches the GPU (no HIP call before the ranks exist); the
+    parent only waits and returns the child's exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", BCG_BENCH_T0=repr(time.time() - (time.perf_counter() - T_PROCESS0)))
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
 
 
 class SimPool:
-    """S independent simulations, each on its own thread, sharing the engine.
+    """S independent games on their own threads, sharing one engine, running until stopped.
 
-    With continuous batching the simulations are NOT in lock-step: one game's
-    retry phase overlaps another game's decide phase, keeping the decode batch
-    full.  A game that ends is replaced by a fresh seed.  ``run(rounds)`` makes
-    every simulation play exactly ``rounds`` rounds.
+    The seed of the game slot ``i`` plays after ``g`` finished games is a pure
+    function of (seed, replica, i, g), so the game sequence is reproducible and
+    identical on every rank that derives it.
     """
 
-    def __init__(self, n_sims, honest, byzantine, max_rounds, seed, rank):
+    def __init__(self, n_sims, honest, byzantine, max_rounds, seed, replica):
         from byzantine_consensus_llm_agents_amd.bcg.simulation import BCGSimulation
         self.BCGSimulation = BCGSimulation
         self.honest, self.byzantine, self.max_rounds = honest, byzantine, max_rounds
-        self.seed_base = seed * 100003 + rank * 7919
-        self.next_seed = 0
+        self.seed_base = seed * 100003 + replica * 7919
         self.lock = threading.Lock()
-        self.sims = [self._new_sim() for _ in range(n_sims)]
+        self.generation = [0] * n_sims
+        self.sims = [self._new_sim(i) for i in range(n_sims)]
+        self.retired = 0          # accepted decisions of games already replaced
         self.games_finished = 0
         self.outcomes = {}
+        self.errors = []
+        self._stop = threading.Event()
+        self.threads = []
 
-    def _new_sim(self):
-        with self.lock:
-            self.next_seed += 1
-            seed = self.seed_base + self.next_seed
+    def _new_sim(self, slot):
+        seed = self.seed_base + slot * 1_000_003 + self.generation[slot]
         return self.BCGSimulation(self.honest, self.byzantine, config={
             "max_rounds": self.max_rounds, "value_range": (0, 50), "consensus_threshold": 66.0,
             "verbose": False, "byzantine_awareness": "may_exist", "seed": seed})
 
-    def run(self, rounds: int, llm=None, lockstep=False) -> int:
-        """Every simulation plays `rounds` rounds; returns accepted decisions."""
-        made = [0] * len(self.sims)
-        errors = []
+    @staticmethod
+    def _made(sim) -> int:
+        return sim.counters["decisions_accepted"] + sim.counters["votes_accepted"]
 
-        def work(i):
-            th = threading.current_thread()
-            th._bcg_participant = lockstep
-            th._bcg_order_key = (i,)
-            try:
-                for _ in range(rounds):
-                    sim = self.sims[i]
-                    before = sim.counters["decisions_accepted"] + sim.counters["votes_accepted"]
-                    sim.run_round()
-                    made[i] += sim.counters["decisions_accepted"] + sim.counters["votes_accepted"] - before
-                    if sim.game.game_over:
-                        o = sim.game.get_statistics().get("consensus_outcome")
-                        with self.lock:
-                            self.outcomes[o] = self.outcomes.get(o, 0) + 1
-                            self.games_finished += 1
-                        self.sims[i] = self._new_sim()
-            except BaseException as exc:  # surface thread failures
-                errors.append(exc)
-            finally:
-                if lockstep:
-                    llm.unregister_client()
+    def accepted(self) -> int:
+        """Accepted decisions so far over every game this pool played (consistent snapshot)."""
+        with self.lock:
+            return self.retired + sum(self._made(s) for s in self.sims)
 
-        if lockstep:
-            for _ in self.sims:
-                llm.register_client()
-        threads = [threading.Thread(target=work, args=(i,)) for i in range(len(self.sims))]
-        for t in threads:
+    def _work(self, i, delay):
+        try:
+            if delay > 0 and self._stop.wait(delay):
+                return
+            while not self._stop.is_set():
+                sim = self.sims[i]
+                sim.run_round()
+                if sim.game.game_over:
+                    o = sim.game.get_statistics().get("consensus_outcome")
+                    self.generation[i] += 1
+                    fresh = self._new_sim(i)
+                    with self.lock:
+                        self.outcomes[o] = self.outcomes.get(o, 0) + 1
+                        self.games_finished += 1
+                        self.retired += self._made(sim)
+                        self.sims[i] = fresh
+        except BaseException as exc:  # surfaced by the main thread
+            self.errors.append(exc)
+
+    def start(self, ramp_s: float = 0.0):
+        n = len(self.sims)
+        for i in range(n):
+            delay = ramp_s * i / n if n > 1 else 0.0
+            t = threading.Thread(target=self._work, args=(i, delay), name=f"sim{i}", daemon=True)
+            self.threads.append(t)
             t.start()
-        for t in threads:
-            t.join()
-        if errors:
-            raise errors[0]
-        return sum(made)
+
+    def stop(self):
+        self._stop.set()
+
+    def check(self):
+        if self.errors:
+            raise self.errors[0]
 
 
-def _heartbeat(llm, stop: threading.Event, every: float = 30.0):
+def _heartbeat(llm, pool, stop: threading.Event, every: float = 30.0):
     """Progress line on stderr every `every` s (long runs must keep writing)."""
     t0 = time.perf_counter()
     while not stop.wait(every):
         st = dict(getattr(llm.backend, "stats", {}))
-        print(f"[progress] {time.perf_counter() - t0:.0f}s {json.dumps(st)}", file=sys.stderr, flush=True)
+        print(f"[progress] {time.perf_counter() - t0:.0f}s accepted={pool.accepted()} {json.dumps(st)}",
+              file=sys.stderr, flush=True)
 
 
-def main():
-    args = parse()
+def main(argv=None):
+    args = parse(argv)
+    world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if world == 0 and args.gpus > 1:
+        sys.exit(self_launch(args))
+    world = max(world, 1)
+    if "BCG_BENCH_T0" in os.environ:  # self-launched rank: the deadline counts from the parent's start
+        t0_wall = float(os.environ["BCG_BENCH_T0"])
+        t_origin = time.perf_counter() - (time.time() - t0_wall)
+    else:
+        t_origin = T_PROCESS0
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and rank == 0:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: measuring {world} rank(s)", file=sys.stderr)
+
     # stdout carries exactly ONE line (the JSON result): anything else -- e.g. the
     # reference's console messages when an agent fails all JSON retries -- goes to stderr
     result_out, sys.stdout = sys.stdout, sys.stderr
     if os.environ.get("BCG_STACKS_AFTER"):  # debugging aid: dump every thread's stack periodically
         import faulthandler
         faulthandler.dump_traceback_later(float(os.environ["BCG_STACKS_AFTER"]), repeat=True, file=sys.stderr)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.backend == "hip":
+
+    import torch
+    import torch.distributed as dist
+
+    gpu = args.backend == "hip"
+    ctrl = None
+    if gpu:
         torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl" if args.backend == "hip" else "gloo")
+        import datetime
+        dist.init_process_group("nccl" if gpu else "gloo", timeout=datetime.timedelta(seconds=900))
+        # control plane (barriers, result reduction) on a CPU group: never queued on a
+        # HIP stream behind the engine's kernels / TP collectives
+        ctrl = dist.new_group(backend="gloo") if gpu else dist.group.WORLD
 
     from byzantine_consensus_llm_agents_amd.bcg import config as C
     from byzantine_consensus_llm_agents_amd.bcg.engine_agent import EngineAgent
@@ -163,11 +225,12 @@ def main():
     from byzantine_consensus_llm_agents_amd.models.config import ALIASES
 
     model = ALIASES.get(args.model, args.model)
+    replica = rank // args.tp
     C.METRICS_CONFIG["save_results"] = False
     C.VLLM_CONFIG["model_name"] = model
     C.VLLM_CONFIG["tensor_parallel_size"] = args.tp
     C.VLLM_CONFIG["quantization"] = args.quantization
-    C.ENGINE_CONFIG.update(backend=args.backend, budget_aware_json=True, seed=args.seed + rank // args.tp,
+    C.ENGINE_CONFIG.update(backend=args.backend, budget_aware_json=True, seed=args.seed + replica,
                            use_hip_graphs=not args.no_graphs, prefix_caching=not args.no_prefix_cache,
                            overlap_prefill=args.overlap_prefill, custom_allreduce=not args.no_custom_allreduce,
                            kv_cache_dtype=args.kv_cache_dtype)
@@ -177,7 +240,7 @@ def main():
     t0 = time.perf_counter()
     llm = LLM(model, max_model_len=C.VLLM_CONFIG["max_model_len"],
               gpu_memory_utilization=C.VLLM_CONFIG["gpu_memory_utilization"],
-              tensor_parallel_size=args.tp, backend=args.backend, seed=args.seed + rank // args.tp,
+              tensor_parallel_size=args.tp, backend=args.backend, seed=args.seed + replica,
               quantization=args.quantization)
     # share the engine with every agent (same model name + config => no reload)
     EngineAgent._shared_llm = llm
@@ -185,56 +248,83 @@ def main():
     EngineAgent._shared_model_config = dict(C.VLLM_CONFIG)
     init_s = time.perf_counter() - t0
 
+    def barrier():
+        if world > 1:
+            dist.barrier(group=ctrl)
+
+    from byzantine_consensus_llm_agents_amd.bcg.prompts import all_schemas
+    llm.precompile(all_schemas(0, 50))  # every rank, same order: identical FSM row bases
+    pool = None
+    if llm.is_driver:
+        llm.start_continuous_batching()
+        pool = SimPool(args.sims_per_gpu, args.honest, args.byzantine, args.max_rounds, args.seed, replica)
+        ramp = args.ramp_s if args.ramp_s is not None else 0.5 * args.warmup * args.window_s
+        pool.start(ramp_s=ramp)
+    else:
+        llm.start_worker()  # TP follower: executes the group driver's plans until it stops
+
     stop_hb = threading.Event()
     if rank == 0:
-        threading.Thread(target=_heartbeat, args=(llm, stop_hb), daemon=True).start()
-    lockstep = args.tp > 1  # TP ranks need identical batches: coalesced lock-step rounds
-    if not lockstep:
-        llm.start_continuous_batching()
-    pool = SimPool(args.sims_per_gpu, args.honest, args.byzantine, args.max_rounds,
-                   args.seed + rank // args.tp, rank // args.tp)
-    if args.warmup:
-        n = pool.run(args.warmup, llm, lockstep)
-        if rank == 0:
-            print(f"[warmup] {args.warmup} rounds/sim, decisions={n}", file=sys.stderr, flush=True)
+        threading.Thread(target=_heartbeat, args=(llm, pool, stop_hb), daemon=True).start()
+
+    def accepted():
+        if pool is None:
+            return 0
+        pool.check()
+        return pool.accepted()
+
+    time.sleep(args.window_s * args.warmup)
+    if rank == 0:
+        print(f"[warmup] {args.warmup} x {args.window_s}s windows, accepted={accepted()} "
+              f"init={init_s:.1f}s", file=sys.stderr, flush=True)
 
     eng = getattr(llm.backend, "stats", {})
     stats0 = dict(eng)
-    if world > 1:
-        dist.barrier()
-    if args.backend == "hip":
+    barrier()
+    if gpu:
         torch.cuda.synchronize()
     t_start = time.perf_counter()
-    decisions = pool.run(args.steps, llm, lockstep)
-    if rank == 0:
-        print(f"[timed] {args.steps} rounds/sim decisions={decisions} elapsed={time.perf_counter() - t_start:.2f}s",
-              file=sys.stderr, flush=True)
-    if args.backend == "hip":
+    a0 = accepted()
+    per_window, steps_done, last = [], 0, a0
+    # the deadline is agreed on by every rank (the slowest start wins)
+    budget = torch.tensor([args.deadline_s - (t_start - t_origin)], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(budget, op=dist.ReduceOp.MIN, group=ctrl)
+    max_windows = max(1, min(args.steps, int(float(budget[0]) // args.window_s)))
+    for k in range(max_windows):
+        delay = t_start + (k + 1) * args.window_s - time.perf_counter()
+        if delay > 0:
+            time.sleep(delay)
+        now = accepted()
+        per_window.append(now - last)
+        last = now
+        steps_done += 1
+    decisions = last - a0
+    if gpu:
         torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    barrier()
     elapsed = time.perf_counter() - t_start
+    if rank == 0:
+        print(f"[timed] {steps_done} windows decisions={decisions} elapsed={elapsed:.2f}s", file=sys.stderr,
+              flush=True)
 
-    # DP groups: only one rank per TP group contributes decisions
-    mine = decisions if rank % args.tp == 0 else 0
+    # DP replicas: only the group driver's pool counts (TP followers run no games)
     if world > 1:
-        t = torch.tensor([mine, elapsed], dtype=torch.float64,
-                         device="cuda" if args.backend == "hip" else "cpu")
-        tot = t.clone()
-        dist.all_reduce(tot[:1], op=dist.ReduceOp.SUM)
-        mx = t[1:].clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        t = torch.tensor([float(decisions), elapsed], dtype=torch.float64)
+        tot, mx = t[:1].clone(), t[1:].clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=ctrl)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=ctrl)
         total_decisions, elapsed = float(tot[0]), float(mx[0])
     else:
-        total_decisions = float(mine)
+        total_decisions = float(decisions)
     value = total_decisions / elapsed if elapsed > 0 else 0.0
     d_eng = {k: eng.get(k, 0) - stats0.get(k, 0) for k in eng}
     if rank == 0:
         line = {
             "metric": f"agent decisions/sec (node), {args.honest}h+{args.byzantine}b BCG {model.split('/')[-1]}; "
                       "consensus-rate parity",
-            "value": round(value, 3), "unit": "decisions/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / max(args.steps, 1), 2),
+            "value": round(value, 3), "unit": "decisions/s", "n_gpus": world, "steps": steps_done,
+            "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / max(steps_done, 1), 2),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": "fp8" if args.quantization == "fp8" else "bf16",
@@ -245,19 +335,27 @@ def main():
                        "sims_per_gpu": args.sims_per_gpu, "seq_len": C.VLLM_CONFIG["max_model_len"],
                        "max_tokens_decide": C.LLM_CONFIG["max_tokens_decide"],
                        "max_tokens_vote": C.LLM_CONFIG["max_tokens_vote"],
+                       "step": f"{args.window_s:g} s window of the continuously-batched pool",
                        "parallelism": f"dp{world // args.tp}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
                        "hip_graphs": not args.no_graphs, "prefix_caching": not args.no_prefix_cache,
                        "overlap_prefill": args.overlap_prefill,
                        "custom_allreduce": args.tp > 1 and not args.no_custom_allreduce},
             "detail": {"decisions": total_decisions, "elapsed_s": round(elapsed, 3), "init_s": round(init_s, 1),
-                       "engine_per_rank": d_eng, "games_finished_rank0": pool.games_finished,
-                       "outcomes_rank0": pool.outcomes,
+                       "steps_requested": args.steps, "window_s": args.window_s,
+                       "decisions_per_window_rank0": per_window,
+                       "engine_per_rank": d_eng, "games_finished_rank0": pool.games_finished if pool else 0,
+                       "outcomes_rank0": pool.outcomes if pool else {},
+                       "wall_since_start_s": round(time.perf_counter() - t_origin, 1),
                        "phases_rank0": llm.backend.timer.summary() if hasattr(llm.backend, "timer") else {}},
         }
         print(json.dumps(line), file=result_out, flush=True)
     stop_hb.set()
+    if pool is not None:
+        pool.stop()
+    # game threads still waiting on the engine are daemons: they die with the process
     llm.shutdown()
     if world > 1:
+        barrier()
         dist.destroy_process_group()
 
 

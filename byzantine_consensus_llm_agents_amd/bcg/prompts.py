@@ -55,6 +55,12 @@ def vote_schema(options: Tuple[str, ...]) -> Dict:
 HONEST_VOTE_OPTIONS = ("stop", "continue")
 BYZANTINE_VOTE_OPTIONS = ("stop", "continue", "abstain")
 
+
+def all_schemas(lo: int, hi: int) -> List[Dict]:
+    """The four agent-output schemas of a game with value range [lo, hi] (engine precompile)."""
+    return [honest_decision_schema(lo, hi), byzantine_decision_schema(lo, hi),
+            vote_schema(HONEST_VOTE_OPTIONS), vote_schema(BYZANTINE_VOTE_OPTIONS)]
+
 # ---------------------------------------------------------- system prompts
 
 _EXECUTION_COMMON = (

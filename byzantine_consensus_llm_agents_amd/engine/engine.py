@@ -18,15 +18,38 @@
 Heterogeneous JSON schemas, temperatures and max_tokens coexist in one batch:
 they are per-row device state (``fsm_base/fsm_state``, ``temperature``,
 ``max_new``).
+
+Threads.  ``submit`` (any caller thread) only does CPU work -- tokenise,
+compile the schema's token FSM -- and appends to ``_incoming``.  Everything
+that touches the device or the schedule runs on ONE scheduler thread (the
+background thread in async mode): each iteration first drains ``_incoming``
+into the admission queue and installs new FSM tables, so the admission order
+and the FSM row bases are decided in one place.
+
+Tensor parallelism (driver / follower).  In a TP group only rank 0 (the
+driver) owns requests and makes scheduling decisions; the other ranks are
+followers that hold their weight shards and replay the driver's schedule.
+Every iteration the driver broadcasts a small plan over a CPU (gloo) group --
+the requests it drained this iteration (token ids, limits, schema) and the one
+timing-dependent decision (launch the next burst before reaping) -- and each
+follower applies it to its own identical engine state.  Everything else
+(admission, KV blocks, compaction, buckets, sampling) is a deterministic
+function of that plan sequence and of device data that is bitwise identical on
+every rank (identical all-reduce / all-gather results, counter-based sampling),
+so all ranks launch the same forwards and collectives in the same order while
+the driver keeps iteration-level continuous batching (the vLLM ``mp``
+executor's model: ``bcg/vllm_agent.py:139-142``).
 """
 
 import collections
 import contextlib
+import json
 import os
 import threading
 from dataclasses import dataclass, field
 from typing import Deque, Dict, List, Optional
 
+import numpy as np
 import torch
 
 from ..bcg.config import ENGINE_CONFIG
@@ -110,7 +133,8 @@ class _Seq:
     prompt_ids: List[int]
     max_new: int
     temperature: float
-    fsm_base: int
+    fsm_key: Optional[str]          # compiled schema key (None = unguided)
+    fsm_base: int = -1              # device row base, assigned by the scheduler thread
     blocks: List[int] = field(default_factory=list)
     cached: int = 0
     error: Optional[str] = None
@@ -124,15 +148,16 @@ class InferenceEngine:
                       "decode_steps": 0, "prefill_chunks": 0, "calls": 0}
         cfg = args.model_cfg
         self.backend = args.backend
+        if self.backend == "hip" and not torch.cuda.is_available():
+            raise RuntimeError("hip backend requested but no GPU is visible")
+        # TP first: joining the process group selects this rank's GPU (LOCAL_RANK)
+        self.tp = self._init_tp(args.tensor_parallel_size)
         if args.device:
             self.device = torch.device(args.device)
         elif self.backend == "hip":
-            if not torch.cuda.is_available():
-                raise RuntimeError("hip backend requested but no GPU is visible")
             self.device = torch.device("cuda", torch.cuda.current_device())
         else:
             self.device = torch.device("cpu")
-        self.tp = self._init_tp(args.tensor_parallel_size)
         self.ops = get_ops(self.backend)
 
         model_dir = args.weights if args.weights not in ("random", "auto") else None
@@ -164,8 +189,14 @@ class InferenceEngine:
             self._load_tuned_gemms()
         self._alloc_state()
         self._cv = threading.Condition()
-        self._waiting: Deque[_Request] = collections.deque()
+        self._incoming: List[_Request] = []        # submitted, not yet seen by the scheduler
+        self._waiting: Deque[_Request] = collections.deque()  # admission queue (scheduler thread)
+        self.is_driver = self.tp.rank == 0
         self.async_mode = False
+        self._follower = None
+        self._fatal: Optional[BaseException] = None
+        self._stop = False
+        self._ar_err_host = None
         self.graphs = None
         # Prefill (MFMA-bound GEMMs) runs on a second stream while decode bursts
         # (HBM-bound) keep replaying on the main stream.  Off under TP: RCCL
@@ -290,6 +321,8 @@ class InferenceEngine:
         the background scheduler thread and this call waits for them.  Sync
         mode: the calling thread drives the scheduler until they are done.
         """
+        if not self.is_driver:
+            raise RuntimeError("generate() on a TP follower: only the group's rank 0 serves requests")
         reqs = self.submit(prompts, params_list)
         if self.async_mode:
             for r in reqs:
@@ -303,25 +336,42 @@ class InferenceEngine:
                 raise r.exc
         return [r.text for r in reqs]
 
+    def _make_request(self, p_ids: List[int], max_tokens: int, temperature: float,
+                      fsm_key: Optional[str]) -> "_Request":
+        seq = _Seq(0, list(p_ids), max(1, int(max_tokens)), float(temperature), fsm_key)
+        req = _Request(seq)
+        n, limit = len(p_ids), self.args.max_model_len
+        if n == 0 or n >= limit:
+            req.finish("")  # no room for even one token: the caller sees an unparsable (empty) output
+        else:
+            # generate up to the context limit, as vLLM does (not an empty answer)
+            seq.max_new = min(seq.max_new, limit - n, OUT_WIDTH)
+        return req
+
     def submit(self, prompts: List[str], params_list) -> List["_Request"]:
-        """Tokenise + compile schemas on the caller's thread, enqueue for admission."""
+        """Tokenise + compile schemas on the caller's thread (CPU only), hand to the scheduler."""
         with self.timer.phase("tokenize"):
             ids = self.tokenizer.encode_batch(prompts)
         reqs = []
         for p_ids, p in zip(ids, params_list):
             schema = p.guided_decoding.json if p.guided_decoding is not None else None
             with self.timer.phase("fsm_compile"):
-                base = self.fsm.get(schema) if schema is not None else -1
-            seq = _Seq(0, p_ids, max(1, int(p.max_tokens)), float(p.temperature), base)
-            req = _Request(seq, self._bursts)
-            if len(p_ids) == 0 or len(p_ids) + seq.max_new > self.args.max_model_len or seq.max_new > OUT_WIDTH:
-                req.finish("")  # reference behaviour: the caller sees an unparsable (empty) output
-            reqs.append(req)
+                key = self.fsm.compile(schema) if schema is not None else None
+            reqs.append(self._make_request(p_ids, p.max_tokens, p.temperature, key))
         with self._cv:
             self.stats["calls"] += 1
-            self._waiting.extend(r for r in reqs if not r.event.is_set())
+            self._incoming.extend(r for r in reqs if not r.event.is_set())
             self._cv.notify_all()
         return reqs
+
+    def precompile(self, schemas) -> None:
+        """Compile + install schemas up front (before serving): no compile inside the timed
+        region, and TP followers need not compile a schema the first time it arrives."""
+        for schema in schemas:
+            key = self.fsm.compile(schema)
+            if not self.async_mode:
+                with self._device_ctx():
+                    self.fsm.install(key)
 
     def _device_ctx(self):
         return torch.cuda.device(self.device) if self.device.type == "cuda" else contextlib.nullcontext()
@@ -340,10 +390,13 @@ class InferenceEngine:
         with self._device_ctx():
             while True:
                 with self._cv:
-                    while not self._stop and not self._waiting and not any(self.slots):
-                        self._cv.wait()
+                    while not self._stop and not self._incoming and not self._waiting and not any(self.slots):
+                        # TP: an idle driver still heartbeats its followers (an empty plan:
+                        # their receive must not run into the process-group timeout)
+                        if not self._cv.wait(timeout=5.0) and self.tp.size > 1:
+                            break
                     if self._stop:
-                        return
+                        break
                 try:
                     self._iterate()
                 except BaseException as exc:  # fail every pending request loudly
@@ -354,12 +407,19 @@ class InferenceEngine:
                         print(f"[engine] scheduler iteration failed ({self._engine_errors}):", file=sys.stderr)
                         traceback.print_exc(file=sys.stderr)
                     self._fail_all(exc)
+                    if self.tp.size > 1:  # a TP group cannot re-synchronise after a failed iteration
+                        self._stop = True
+                        self._fatal = exc
+                        break
+            if self.tp.size > 1 and self._fatal is None:
+                self._send_plan({"stop": True})
 
     def _fail_all(self, exc):
         self._inflight = None
         self._snap = None
         with self._cv:
-            pending = list(self._waiting)
+            pending = list(self._incoming) + list(self._waiting)
+            self._incoming.clear()
             self._waiting.clear()
         for i, s in enumerate(self.slots):
             if s is not None:
@@ -369,22 +429,93 @@ class InferenceEngine:
             r.exc = exc
             r.event.set()
 
+    # ---- TP plan exchange (driver -> followers, CPU group) ----
+    def _send_plan(self, plan: dict):
+        import torch.distributed as dist
+        dist.broadcast_object_list([plan], src=self.tp.leader, group=self.tp.ctrl)
+
+    def _recv_plan(self) -> dict:
+        import torch.distributed as dist
+        box = [None]
+        dist.broadcast_object_list(box, src=self.tp.leader, group=self.tp.ctrl)
+        return box[0]
+
+    @staticmethod
+    def _pack_requests(reqs: List["_Request"]) -> dict:
+        lens = [len(r.seq.prompt_ids) for r in reqs]
+        ids = np.fromiter((t for r in reqs for t in r.seq.prompt_ids), dtype=np.int32, count=sum(lens))
+        return {"ids": ids, "lens": lens, "max_new": [r.seq.max_new for r in reqs],
+                "temp": [r.seq.temperature for r in reqs], "fsm": [r.seq.fsm_key for r in reqs]}
+
+    def _unpack_requests(self, spec: dict) -> List["_Request"]:
+        reqs, off = [], 0
+        ids = spec["ids"].tolist()
+        for n, m, t, key in zip(spec["lens"], spec["max_new"], spec["temp"], spec["fsm"]):
+            if key is not None:
+                with self.timer.phase("fsm_compile"):
+                    self.fsm.compile(json.loads(key))
+            r = _Request(_Seq(0, ids[off:off + n], m, t, key))
+            off += n
+            reqs.append(r)
+        return reqs
+
+    def serve_follower(self):
+        """TP follower loop: apply the driver's plans until it says stop (blocking)."""
+        with self._device_ctx():
+            while True:
+                plan = self._recv_plan()
+                if plan.get("stop"):
+                    return
+                self._iterate(plan)
+
+    def start_follower(self):
+        """Run `serve_follower` on a background thread (bench / library use)."""
+        if self._follower is None:
+            self._follower = threading.Thread(target=self._follower_main, name="bcg-tp-follower", daemon=True)
+            self._follower.start()
+
+    def _follower_main(self):
+        try:
+            self.serve_follower()
+        except BaseException as exc:  # noqa: BLE001 -- surfaced through `fatal`
+            import sys
+            import traceback
+            print("[engine] TP follower failed:", file=sys.stderr)
+            traceback.print_exc(file=sys.stderr)
+            self._fatal = exc
+
     # ---- one scheduler iteration ----
-    def _iterate(self):
-        """reap -> activate prefills -> admit -> decode burst -> snapshot.
+    def _iterate(self, plan: Optional[dict] = None):
+        """(TP plan exchange) -> reap -> activate prefills -> admit -> decode burst -> snapshot.
 
         The host never blocks the device between bursts: completion is read
         from a pinned snapshot taken after the previous burst, and while the
         device is still running that burst the next one is queued FIRST (rows
         that finished in it idle one extra burst, harmlessly -- the sampler
-        skips done rows and their blocks are freed only after).  Under TP the
-        early launch is off: it depends on timing, and TP ranks must make
-        identical scheduling decisions.
+        skips done rows and their blocks are freed only after).  That choice
+        depends on timing, so under TP the driver makes it and ships it in the
+        plan; followers (``plan`` given) take it from there.
         """
-        launched = False
         snap = self._snap
-        if (snap is not None and self.tp.size == 1 and snap["event"] is not None
-                and not snap["event"].query() and self._live_rows()):
+        if plan is None:
+            with self._cv:
+                new, self._incoming = self._incoming, []
+            early = bool(snap is not None and snap["event"] is not None and not snap["event"].query()
+                         and self._live_rows())
+            if self.tp.size > 1:
+                self._send_plan({"new": self._pack_requests(new), "early": early})
+        else:
+            new = self._unpack_requests(plan["new"])
+            early = plan["early"]
+        if new:
+            for r in new:  # FSM rows are installed here, in admission order (identical on TP ranks)
+                if r.seq.fsm_key is not None:
+                    r.seq.fsm_base = self.fsm.install(r.seq.fsm_key)
+                r.enq_burst = self._bursts
+            with self._cv:
+                self._waiting.extend(new)
+        launched = False
+        if early and self._live_rows():
             self._decode_burst()
             launched = True
         self._reap()
@@ -417,6 +548,10 @@ class InferenceEngine:
         h["done"][:n].copy_(st["done"][:n], non_blocking=True)
         h["count"][:n].copy_(st["gen_count"][:n], non_blocking=True)
         h["out"][:n].copy_(st["out_tokens"][:n], non_blocking=True)
+        if self.tp.custom is not None:  # the xGMI all-reduce's timeout word rides along
+            if self._ar_err_host is None:
+                self._ar_err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self.tp.custom.error_async(self._ar_err_host, torch.cuda.current_stream())
         event = torch.cuda.Event()
         event.record()
         self._snap = {"rows": rows, "n": n, "event": event, "done": h["done"], "count": h["count"],
@@ -552,6 +687,10 @@ class InferenceEngine:
         if snap["event"] is not None:
             with self.timer.phase("wait_burst"):
                 snap["event"].synchronize()
+            if self._ar_err_host is not None and int(self._ar_err_host[0]):
+                # a TP peer never arrived at an all-reduce barrier: the activations of
+                # this burst are not trustworthy -- fail loudly instead of decoding garbage
+                raise RuntimeError("xGMI all-reduce barrier timed out (a tensor-parallel peer stalled or died)")
         n = snap["n"]
         done = snap["done"][:n].tolist()
         finished = [i for i in snap["rows"] if done[i]]
@@ -722,8 +861,13 @@ class InferenceEngine:
             with self._cv:
                 self._stop = True
                 self._cv.notify_all()
-            self._thread.join(timeout=30)
+            self._thread.join(timeout=120)  # the TP driver's loop sends the followers' stop
             self.async_mode = False
+        elif self.tp.size > 1 and self.is_driver and self.model is not None and self._fatal is None:
+            self._send_plan({"stop": True})  # sync-mode driver: release the followers
+        if self._follower is not None:
+            self._follower.join(timeout=120)
+            self._follower = None
         self.graphs = None
         self.k_cache = self.v_cache = None
         self.model = None

@@ -80,6 +80,9 @@ class DecodeGraphs:
         e = self.engine
         if self.version != e.fsm.version:
             self.graphs.clear()
+            # no graph references the old FSM tables any more; replays still in flight
+            # finish before anything re-uses that memory (same stream, stream-ordered allocator)
+            e.fsm.release_retired()
             self.version = e.fsm.version
             if e.args.precapture_graphs:
                 self.capture_all(e.state["done"].shape[0])

@@ -35,7 +35,7 @@ class CompiledFSM:
 def compile_schema(schema: Dict, token_bytes: List[bytes], vocab_rows: int, max_ws: int = 4,
                    native: bool = True) -> CompiledFSM:
     dfa = schema_to_dfa(schema, max_ws=max_ws)
-    key = json.dumps(schema, sort_keys=True)
+    key = FSMRegistry.key_of(schema)
     if native:
         from ...runtime import compile_token_fsm
         nxt, dist = compile_token_fsm(dfa.trans, dfa.accept.astype(np.uint8), token_bytes, vocab_rows)
@@ -76,7 +76,21 @@ def compile_token_fsm_py(trans: np.ndarray, accept: np.ndarray, token_bytes: Lis
 
 
 class FSMRegistry:
-    """Compiles schemas on first use and keeps all tables resident on the device."""
+    """Compiles schemas on first use and keeps all tables resident on the device.
+
+    Two halves with different owners:
+
+    * ``compile(schema)`` -- the CPU work (schema -> byte DFA -> token table), on
+      any thread (the simulation threads call it from ``submit``); cached by key,
+      lock-free on a hit;
+    * ``install(key)`` -- copies a compiled table into the packed device tensor
+      and returns its row base.  Called ONLY by the thread that launches decode
+      work (the engine's scheduler), between bursts: a re-allocation can then
+      never race a graph replay that still reads the old tensor, and the bases
+      are assigned in the scheduler's (deterministic) admission order, so TP
+      ranks agree on them.  Re-allocated tables stay alive in ``retired`` until
+      the decode graphs that captured them are re-captured.
+    """
 
     def __init__(self, token_bytes: List[bytes], vocab_rows: int, device, max_ws: int = 4,
                  native: bool = True):
@@ -93,45 +107,61 @@ class FSMRegistry:
         self.dist = torch.full((1,), 0, dtype=torch.int16, device=self.device)
         self.rows = 0
         self.version = 0  # bumped whenever `table`/`dist` are re-allocated (graphs must re-capture)
+        self.retired: List[tuple] = []  # old (table, dist) pairs, kept until graphs re-capture
 
     @staticmethod
     def key_of(schema: Dict) -> str:
-        return json.dumps(schema, sort_keys=True)
+        # NOT sort_keys: property order is part of the grammar (the order the JSON object's
+        # fields are generated in), and the key must round-trip (json.loads) to the same
+        # schema -- TP followers rebuild the FSM from it
+        return json.dumps(schema, separators=(",", ":"))
 
-    def get(self, schema: Dict) -> int:
+    def compile(self, schema: Dict) -> str:
+        """CPU compile (any thread); returns the schema key for `install`."""
         key = self.key_of(schema)
-        # hit path without the lock: `_bases[key]` is published only after the rows are
-        # written, and a dict read is atomic, so callers no longer queue behind a compile
+        if key in self._fsms:  # lock-free hit: entries are published fully built
+            return key
+        with self._lock:
+            if key not in self._fsms:
+                self._fsms[key] = compile_schema(schema, self.token_bytes, self.vocab_rows, self.max_ws,
+                                                 self.native)
+        return key
+
+    def install(self, key: str) -> int:
+        """Device rows of a compiled schema (scheduler thread only); returns the row base."""
         base = self._bases.get(key)
         if base is not None:
             return base
-        with self._lock:
-            base = self._bases.get(key)
-            if base is not None:
-                return base
-            fsm = compile_schema(schema, self.token_bytes, self.vocab_rows, self.max_ws, self.native)
-            base = self.rows
-            new_rows = self.rows + fsm.num_states
-            if new_rows > self.capacity:
-                # geometric growth keeps re-allocations (and graph re-captures) rare
-                cap = max(new_rows, 2 * self.capacity, 512)
-                table = torch.full((cap, self.vocab_rows), -1, dtype=torch.int16, device=self.device)
-                dist = torch.zeros((cap,), dtype=torch.int16, device=self.device)
-                if self.rows:
-                    table[:self.rows] = self.table[:self.rows]
-                    dist[:self.rows] = self.dist[:self.rows]
-                self.table, self.dist, self.capacity = table, dist, cap
-                self.version += 1
-            self.table[base:new_rows] = torch.from_numpy(fsm.next).to(self.device)
-            self.dist[base:new_rows] = torch.from_numpy(fsm.dist).to(self.device)
-            self.rows = new_rows
-            self._bases[key] = base
-            self._fsms[key] = fsm
-            return base
+        fsm = self._fsms[key]
+        base = self.rows
+        new_rows = self.rows + fsm.num_states
+        if new_rows > self.capacity:
+            # geometric growth keeps re-allocations (and graph re-captures) rare
+            cap = max(new_rows, 2 * self.capacity, 512)
+            table = torch.full((cap, self.vocab_rows), -1, dtype=torch.int16, device=self.device)
+            dist = torch.zeros((cap,), dtype=torch.int16, device=self.device)
+            if self.rows:
+                table[:self.rows] = self.table[:self.rows]
+                dist[:self.rows] = self.dist[:self.rows]
+            self.retired.append((self.table, self.dist))
+            self.table, self.dist, self.capacity = table, dist, cap
+            self.version += 1
+        self.table[base:new_rows] = torch.from_numpy(fsm.next).to(self.device)
+        self.dist[base:new_rows] = torch.from_numpy(fsm.dist).to(self.device)
+        self.rows = new_rows
+        self._bases[key] = base
+        return base
+
+    def release_retired(self):
+        """The decode graphs were re-captured against the current table: old ones may go."""
+        self.retired.clear()
+
+    def get(self, schema: Dict) -> int:
+        """compile + install in one call (single-threaded users: tests, tools)."""
+        return self.install(self.compile(schema))
 
     def fsm(self, schema: Dict) -> CompiledFSM:
-        self.get(schema)
-        return self._fsms[self.key_of(schema)]
+        return self._fsms[self.compile(schema)]
 
     def start_dist(self, base: int) -> int:
         return int(self.dist[base].item())

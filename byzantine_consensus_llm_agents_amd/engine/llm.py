@@ -11,8 +11,15 @@ Backends:
   * ``torch`` - the same engine on PyTorch reference ops (CPU tests);
   * ``fake``  - scripted schema-valid answers (plumbing, parity tests).
 
+Tensor parallelism: ``tensor_parallel_size > 1`` in a process that was not
+started by a launcher spawns the TP worker processes itself (ranks 1..N-1, each
+running :mod:`.tp_worker`), like vLLM's ``mp`` executor; this process becomes
+the group's driver.  Under an external launcher (torchrun) every rank builds
+the same ``LLM``; ``is_driver`` tells the group's rank 0 (serves requests) from
+the followers (``serve_worker`` / ``start_worker``).
+
 Several simulations may share one ``LLM`` from different threads.  With
-``start_continuous_batching()`` (TP = 1) every call's sequences join the
+``start_continuous_batching()`` every call's sequences join the
 engine's running decode batch as soon as they arrive and leave it when they
 finish (iteration-level scheduling).  Otherwise calls are coalesced
 (:class:`Coalescer`) into one batch once every registered thread waits on the
@@ -143,10 +150,22 @@ class LLM:
         self.model = model
         self.backend_name = resolve_backend(backend)
         seed = seed if seed is not None else ENGINE_CONFIG.get("seed")
+        self.workers = None
         if self.backend_name == "fake":
             from .fake import FakeBackend
             self.backend = FakeBackend(seed=seed or 0)
+            # scripted engine: no model to shard; under a TP layout only each group's rank 0 serves
+            self.backend.is_driver = int(os.environ.get("RANK", "0")) % max(1, tensor_parallel_size) == 0
         elif self.backend_name in ("hip", "torch"):
+            if tensor_parallel_size > 1:
+                # the reference's entry point gets TP workers from vLLM's 'mp' executor
+                # (bcg/vllm_agent.py:139-142); here: spawn them unless a launcher did
+                from ..parallel.launcher import spawn_tp_workers
+                self.workers = spawn_tp_workers(tensor_parallel_size, dict(
+                    model=model, max_model_len=max_model_len, gpu_memory_utilization=gpu_memory_utilization,
+                    tensor_parallel_size=tensor_parallel_size, max_num_seqs=max_num_seqs,
+                    quantization=quantization, backend=self.backend_name, weights=weights, seed=seed,
+                    **kwargs))
             from .engine import EngineArgs, InferenceEngine
             args = EngineArgs.from_configs(model, max_model_len=max_model_len,
                                            gpu_memory_utilization=gpu_memory_utilization,
@@ -207,10 +226,33 @@ class LLM:
             self._next_id += 1
         return outs
 
+    @property
+    def is_driver(self) -> bool:
+        """False on a TP follower rank (it serves no requests, it replays the driver's plans)."""
+        return getattr(self.backend, "is_driver", True)
+
     def start_continuous_batching(self):
-        """Switch the engine to its background scheduler (DP / TP=1 serving)."""
+        """Switch the engine to its background scheduler (iteration-level batching; TP drivers too)."""
         if hasattr(self.backend, "start_async"):
             self.backend.start_async()
 
+    def start_worker(self):
+        """TP follower: replay the driver's plans on a background thread until it stops."""
+        if hasattr(self.backend, "start_follower"):
+            self.backend.start_follower()
+
+    def serve_worker(self):
+        """TP follower: replay the driver's plans on this thread until it stops (blocking)."""
+        if hasattr(self.backend, "serve_follower"):
+            self.backend.serve_follower()
+
+    def precompile(self, schemas):
+        """Compile JSON-schema FSMs up front (no-op for the scripted backend)."""
+        if hasattr(self.backend, "precompile"):
+            self.backend.precompile(schemas)
+
     def shutdown(self):
         self.backend.shutdown()
+        if self.workers is not None:
+            self.workers.join()
+            self.workers = None

@@ -48,8 +48,10 @@ class TPGroup:
     accepts -- the decode-sized ones; the rest go through RCCL.
     """
 
-    def __init__(self, group=None, rank: int = 0, size: int = 1, custom=None):
+    def __init__(self, group=None, rank: int = 0, size: int = 1, custom=None, ctrl=None, leader: int = 0):
         self.group, self.rank, self.size, self.custom = group, rank, size, custom
+        self.ctrl = ctrl        # CPU (gloo) group of the same ranks: the driver's plan broadcasts
+        self.leader = leader    # global rank of this group's rank 0 (the driver)
 
     def all_reduce_(self, x: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
@@ -109,73 +111,93 @@ class DecoderModel:
         return shapes
 
     def init_random(self, seed: int = 0, std: float = 0.02):
-        """Random-init weights of this rank's shard directly on the device."""
-        gen = torch.Generator(device=self.device)
-        gen.manual_seed(seed * 1000003 + self.tp.rank)
-        c = self.cfg
+        """Random-init weights, identical for every TP degree.
 
-        def normal(*shape):
+        Each full (unsharded) tensor is drawn from its own seeded generator and
+        then sliced exactly like a checkpoint (`_load_layer`), so a TP=2 engine
+        holds the two halves of the TP=1 engine's weights (TP-vs-TP=1 parity
+        tests, and every rank derives its shard without communication).
+        """
+        c, hd, H = self.cfg, self.hd, self.cfg.hidden_size
+        gen = torch.Generator(device=self.device)
+
+        def normal(shape, tag):
+            gen.manual_seed((seed * 1000003 + tag * 7919 + 17) & 0x7FFFFFFFFFFFFFFF)
             t = torch.empty(*shape, device=self.device, dtype=self.dtype)
             t.normal_(0.0, std, generator=gen)
             return t
 
-        def ones(*shape):
-            return torch.ones(*shape, device=self.device, dtype=self.dtype)
+        def ones(n):
+            return torch.ones(n, device=self.device, dtype=self.dtype)
 
+        full = {"self_attn.q_proj.weight": (c.num_heads * hd, H), "self_attn.k_proj.weight": (c.num_kv_heads * hd, H),
+                "self_attn.v_proj.weight": (c.num_kv_heads * hd, H), "self_attn.o_proj.weight": (H, c.num_heads * hd),
+                "mlp.gate_proj.weight": (c.intermediate_size, H), "mlp.up_proj.weight": (c.intermediate_size, H),
+                "mlp.down_proj.weight": (H, c.intermediate_size)}
+        if c.qkv_bias:
+            full.update({"self_attn.q_proj.bias": (c.num_heads * hd,), "self_attn.k_proj.bias": (c.num_kv_heads * hd,),
+                         "self_attn.v_proj.bias": (c.num_kv_heads * hd,)})
         self.layers = []
-        for _ in range(c.num_layers):
-            layer = {}
-            for name, shape in self._shapes().items():
-                layer[name] = ones(*shape) if name in ("ln1", "ln2", "q_norm", "k_norm") else normal(*shape)
-            self.layers.append(layer)
-        # embedding replicated on every TP rank (1.5 GB bf16 at 152k x 5120); head vocab-parallel
-        g0 = torch.Generator(device=self.device)
-        g0.manual_seed(seed * 1000003 + 7)
-        self.embed = torch.empty(c.vocab_size, c.hidden_size, device=self.device, dtype=self.dtype)
-        self.embed.normal_(0.0, std, generator=g0)
+        for i in range(c.num_layers):
+            tensors = {name: normal(shape, 64 * i + j) for j, (name, shape) in enumerate(full.items())}
+            tensors["input_layernorm.weight"] = ones(H)
+            tensors["post_attention_layernorm.weight"] = ones(H)
+            if c.qk_norm:
+                tensors["self_attn.q_norm.weight"] = ones(hd)
+                tensors["self_attn.k_norm.weight"] = ones(hd)
+            self.layers.append(self._load_layer(tensors.__getitem__))
+            del tensors
+        self.embed = normal((c.vocab_size, H), 1 << 20)
         if c.tie_embeddings:
             lo = self.tp.rank * self.vocab_local
             self.lm_head = self.embed[lo:lo + self.vocab_local]
         else:
-            self.lm_head = normal(self.vocab_local, c.hidden_size)
-        self.final_norm = ones(c.hidden_size)
+            head = normal((c.vocab_size, H), (1 << 20) + 1)
+            lo = self.tp.rank * self.vocab_local
+            self.lm_head = head[lo:lo + self.vocab_local].contiguous()
+            del head
+        self.final_norm = ones(H)
         self._finish()
 
-    def load_hf_state_dict(self, sd: Dict[str, torch.Tensor]):
-        """Load (and TP-slice) an HF-named state dict (Qwen2/Qwen3/Mistral naming)."""
-        c, r = self.cfg, self.tp.rank
-        hd = self.hd
-
-        def get(name):
-            return sd[name].to(device=self.device, dtype=self.dtype)
+    def _load_layer(self, get) -> Dict[str, torch.Tensor]:
+        """This rank's shard of one decoder layer from HF-named full tensors (`get(name)`):
+        column-parallel q/k/v and gate/up (row blocks), row-parallel o/down (column blocks)."""
+        c, r, hd = self.cfg, self.tp.rank, self.hd
 
         def rows(t, n_local, per=1):
             return t[r * n_local * per:(r + 1) * n_local * per]
 
-        self.layers = []
-        for i in range(c.num_layers):
-            p = f"model.layers.{i}."
-            q = rows(get(p + "self_attn.q_proj.weight"), self.n_q, hd)
-            k = rows(get(p + "self_attn.k_proj.weight"), self.n_kv, hd)
-            v = rows(get(p + "self_attn.v_proj.weight"), self.n_kv, hd)
-            layer = {"qkv": torch.cat([q, k, v]).contiguous(),
-                     "o": get(p + "self_attn.o_proj.weight")[:, r * self.n_q * hd:(r + 1) * self.n_q * hd].contiguous(),
-                     "gate_up": torch.cat([rows(get(p + "mlp.gate_proj.weight"), self.inter),
-                                           rows(get(p + "mlp.up_proj.weight"), self.inter)]).contiguous(),
-                     "down": get(p + "mlp.down_proj.weight")[:, r * self.inter:(r + 1) * self.inter].contiguous(),
-                     "ln1": get(p + "input_layernorm.weight"),
-                     "ln2": get(p + "post_attention_layernorm.weight")}
-            if c.qkv_bias:
-                layer["qkv_bias"] = torch.cat([rows(get(p + "self_attn.q_proj.bias"), self.n_q, hd),
-                                               rows(get(p + "self_attn.k_proj.bias"), self.n_kv, hd),
-                                               rows(get(p + "self_attn.v_proj.bias"), self.n_kv, hd)])
-            if c.qk_norm:
-                layer["q_norm"] = get(p + "self_attn.q_norm.weight")
-                layer["k_norm"] = get(p + "self_attn.k_norm.weight")
-            self.layers.append(layer)
+        q = rows(get("self_attn.q_proj.weight"), self.n_q, hd)
+        k = rows(get("self_attn.k_proj.weight"), self.n_kv, hd)
+        v = rows(get("self_attn.v_proj.weight"), self.n_kv, hd)
+        layer = {"qkv": torch.cat([q, k, v]).contiguous(),
+                 "o": get("self_attn.o_proj.weight")[:, r * self.n_q * hd:(r + 1) * self.n_q * hd].contiguous(),
+                 "gate_up": torch.cat([rows(get("mlp.gate_proj.weight"), self.inter),
+                                       rows(get("mlp.up_proj.weight"), self.inter)]).contiguous(),
+                 "down": get("mlp.down_proj.weight")[:, r * self.inter:(r + 1) * self.inter].contiguous(),
+                 "ln1": get("input_layernorm.weight"),
+                 "ln2": get("post_attention_layernorm.weight")}
+        if c.qkv_bias:
+            layer["qkv_bias"] = torch.cat([rows(get("self_attn.q_proj.bias"), self.n_q, hd),
+                                           rows(get("self_attn.k_proj.bias"), self.n_kv, hd),
+                                           rows(get("self_attn.v_proj.bias"), self.n_kv, hd)])
+        if c.qk_norm:
+            layer["q_norm"] = get("self_attn.q_norm.weight")
+            layer["k_norm"] = get("self_attn.k_norm.weight")
+        return layer
+
+    def load_hf_state_dict(self, sd: Dict[str, torch.Tensor]):
+        """Load (and TP-slice) an HF-named state dict (Qwen2/Qwen3/Mistral naming)."""
+        c = self.cfg
+
+        def get(name):
+            return sd[name].to(device=self.device, dtype=self.dtype)
+
+        self.layers = [self._load_layer(lambda n, p=f"model.layers.{i}.": get(p + n)) for i in range(c.num_layers)]
         self.embed = get("model.embed_tokens.weight")
         head = self.embed if c.tie_embeddings or "lm_head.weight" not in sd else get("lm_head.weight")
-        self.lm_head = rows(head, self.vocab_local).contiguous()
+        lo = self.tp.rank * self.vocab_local
+        self.lm_head = head[lo:lo + self.vocab_local].contiguous()
         self.final_norm = get("model.norm.weight")
         self._finish()
 

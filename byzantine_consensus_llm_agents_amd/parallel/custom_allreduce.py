@@ -59,6 +59,8 @@ def _lib():
            "bcg_ar_ipc_open": [vp, P],
            "bcg_ar_ipc_close": [vp],
            "bcg_ar_take_error": [vp],
+           "bcg_ar_error_async": [vp, vp, vp],
+           "bcg_ar_set_error": [vp],
            "bcg_ar_allreduce": [P, P, c_int, c_int, vp, vp, c_int64, c_int64, c_int, c_int, c_double, vp]}
     for name, argtypes in sig.items():
         fn = getattr(lib, name)
@@ -105,6 +107,17 @@ class _Rank:
             raise RuntimeError(f"bcg_ar_allreduce launch failed (rc={rc})")
         self.calls[mode] += 1
         return out
+
+    def error_async(self, host: torch.Tensor, stream) -> None:
+        """Queue a copy of this rank's error word into pinned int32 `host[0]` on `stream`."""
+        if self.lib.bcg_ar_error_async(self._sig[self.rank], ctypes.c_void_p(host.data_ptr()),
+                                       ctypes.c_void_p(stream.cuda_stream)) != 0:
+            raise RuntimeError("bcg_ar_error_async failed")
+
+    def set_error(self) -> None:
+        """Mark this rank's group broken (tests of the timeout path)."""
+        if self.lib.bcg_ar_set_error(self._sig[self.rank]) != 0:
+            raise RuntimeError("bcg_ar_set_error failed")
 
     def take_error(self) -> bool:
         """True if a barrier of this rank timed out since the last check (synchronising)."""

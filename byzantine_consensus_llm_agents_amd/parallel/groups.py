@@ -51,6 +51,7 @@ class Layout:
 
 
 _TP_GROUPS = {}
+_TP_CTRL = {}
 _DP_GROUPS = {}
 _CUSTOM_AR = {}
 
@@ -101,13 +102,17 @@ def tensor_parallel_group(tp: int, custom_allreduce: bool = False) -> TPGroup:
     if dist.get_world_size() != lay.world:
         lay = Layout(dist.get_world_size(), dist.get_rank(), lay.local_rank, tp)
     if tp not in _TP_GROUPS:
-        mine = None
+        mine = ctrl = None
+        gloo = dist.get_backend() == "gloo"
         for g in range(lay.world // tp):  # new_group is collective over ALL ranks
             ranks = list(range(g * tp, (g + 1) * tp))
             pg = dist.new_group(ranks)
+            # the driver's scheduling plans travel over CPU: never queued on a HIP stream
+            cg = pg if gloo else dist.new_group(ranks, backend="gloo")
             if lay.rank in ranks:
-                mine = pg
+                mine, ctrl = pg, cg
         _TP_GROUPS[tp] = mine
+        _TP_CTRL[tp] = ctrl
     custom = None
     mode = os.environ.get("BCG_CUSTOM_AR", "1")  # 0 = RCCL only, force = also over gloo (1-GPU tests)
     if custom_allreduce and mode != "0" and (mode == "force" or dist.get_backend(_TP_GROUPS[tp]) == "nccl"):
@@ -115,7 +120,8 @@ def tensor_parallel_group(tp: int, custom_allreduce: bool = False) -> TPGroup:
             from .custom_allreduce import XGMIAllReduce
             _CUSTOM_AR[tp] = XGMIAllReduce(_TP_GROUPS[tp])
         custom = _CUSTOM_AR[tp]
-    return TPGroup(_TP_GROUPS[tp], lay.tp_rank, tp, custom=custom)
+    return TPGroup(_TP_GROUPS[tp], lay.tp_rank, tp, custom=custom, ctrl=_TP_CTRL[tp],
+                   leader=lay.rank - lay.tp_rank)
 
 
 def data_parallel_group(tp: int):
@@ -135,6 +141,7 @@ def destroy():
         ar.close()
     _CUSTOM_AR.clear()
     _TP_GROUPS.clear()
+    _TP_CTRL.clear()
     _DP_GROUPS.clear()
     if dist.is_initialized():
         dist.destroy_process_group()

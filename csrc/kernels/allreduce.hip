@@ -75,7 +75,10 @@ __device__ __forceinline__ void ar_wait(const ArPeers& P, int rank, int world, i
                                         uint64_t timeout_ticks) {
   const int t = threadIdx.x;
   if (t < WAVE) {
-    if (t < world && t != rank) {
+    // once any barrier of this rank timed out the group is broken: do not wait again
+    // (the grid drains at once; the host reads the error word after the burst and raises)
+    const bool broken = __hip_atomic_load(&P.sig[rank]->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+    if (t < world && t != rank && !broken) {
       uint32_t* f = &P.sig[rank]->flags[phase][blockIdx.x][t];
       const uint64_t t0 = wall_clock64();
       // a peer may already be one call ahead: accept any epoch >= ours (wrap-safe)
@@ -252,6 +255,20 @@ BCG_API int bcg_ar_take_error(void* sig) {
     if (hipMemcpy(&s->error, &zero, sizeof(zero), hipMemcpyHostToDevice) != hipSuccess) return -1;
   }
   return static_cast<int>(err);
+}
+
+// Asynchronous copy of a rank's error word into (pinned) host memory on `stream`
+// -- queued after a decode burst, read by the host once the burst's event fired.
+BCG_API int bcg_ar_error_async(void* sig, void* host, hipStream_t stream) {
+  ArSignal* s = static_cast<ArSignal*>(sig);
+  return hipMemcpyAsync(host, &s->error, sizeof(uint32_t), hipMemcpyDeviceToHost, stream) == hipSuccess ? 0 : -1;
+}
+
+// Sets a rank's error word (tests: the forced-timeout path).
+BCG_API int bcg_ar_set_error(void* sig) {
+  ArSignal* s = static_cast<ArSignal*>(sig);
+  const uint32_t one = 1;
+  return hipMemcpy(&s->error, &one, sizeof(one), hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
 }
 
 // n: bf16 elements (multiple of 8); mode 1 = one-shot, 2 = two-shot.
