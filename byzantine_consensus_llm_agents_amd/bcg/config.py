@@ -82,7 +82,7 @@ METRICS_CONFIG = {
 ENGINE_CONFIG = {
     "backend": os.environ.get("BCG_ENGINE", "auto"),
     "weights": os.environ.get("BCG_WEIGHTS", "auto"),  # auto | random | <dir with safetensors>
-    "dtype": "bfloat16",
+    "dtype": os.environ.get("BCG_DTYPE", "bfloat16"),  # activation/weight dtype (float32: CPU parity tests)
     "kv_block_size": 16,
     "seed": None,                  # None = unseeded (reference behaviour)
     "budget_aware_json": False,    # force closing JSON before max_tokens

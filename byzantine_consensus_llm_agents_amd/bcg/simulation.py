@@ -119,6 +119,13 @@ def run_concurrently(engine_agent, jobs):
     errors = []
 
     parent_key = getattr(threading.current_thread(), "_bcg_order_key", ())
+    # A participating parent hands its registration to the children and gets it back
+    # from the LAST child to finish (that child does not unregister): the coalescer's
+    # participant count never drops below the threads that will still submit, so a
+    # batch is never flushed without the parent's next ticket.
+    parent = getattr(threading.current_thread(), "_bcg_participant", False)
+    remaining = [len(jobs)]
+    lock = threading.Lock()
 
     def work(i, job):
         threading.current_thread()._bcg_order_key = tuple(parent_key) + (i,)
@@ -127,21 +134,19 @@ def run_concurrently(engine_agent, jobs):
         except BaseException as exc:
             errors.append(exc)
         finally:
-            llm.unregister_client()
+            with lock:
+                remaining[0] -= 1
+                last = remaining[0] == 0
+            if not (parent and last):
+                llm.unregister_client()
 
-    for _ in jobs:
-        llm.register_client()
+    for _ in range(len(jobs) - (1 if parent else 0)):
+        llm.register_client()  # (+ the parent's own registration, handed over)
     threads = [threading.Thread(target=work, args=(i, j)) for i, j in enumerate(jobs)]
     for t in threads:
         t.start()
-    # the calling thread stops counting as a participant while it waits
-    parent = getattr(threading.current_thread(), "_bcg_participant", False)
-    if parent:
-        llm.unregister_client()
     for t in threads:
         t.join()
-    if parent:
-        llm.register_client()
     if errors:
         raise errors[0]
     return results
@@ -270,10 +275,12 @@ class BCGSimulation:
                     results[aid] = res
                 else:
                     failed.append((aid, prompt))
-                    self.log(f"  ⚠️ [{aid}] Invalid response on attempt {attempt}")
+                    what = "response" if kind == "agents" else "vote"
+                    self.log(f"  ⚠️ [{aid}] Invalid {what} on attempt {attempt}")
             pending = failed
             if pending and attempt < MAX_RETRIES and len(pending) / len(jobs) <= BATCH_RETRY_THRESHOLD:
-                self.log(f"  [SEQUENTIAL RETRY] {len(pending)} {kind} failed, retrying individually...")
+                share = f" (<{BATCH_RETRY_THRESHOLD * 100:.0f}%)" if kind == "agents" else ""
+                self.log(f"  [SEQUENTIAL RETRY] {len(pending)} {kind} failed{share}, retrying individually...")
                 pending = sequential(pending, results)
                 break
         return results

@@ -7,9 +7,11 @@ launch covers the whole sweep:
 
 * one process per GPU (``torchrun``), TP groups of ``--tp`` consecutive ranks
   (RCCL + xGMI all-reduce), DP replicas over the groups;
-* every replica plays its share of the seeds (round-robin), ``--concurrency``
-  games at a time on ONE engine -- their decide/vote batches share the
-  continuously-batched decode (TP groups: coalesced lock-step batches);
+* replicas pull seeds one at a time from a node-wide counter (TCPStore), so
+  uneven game lengths never leave a replica idle while another still holds a
+  static share; each replica plays ``--concurrency`` games at a time on ONE
+  engine -- their decide/vote batches share the continuously-batched decode
+  (TP groups: the group's rank 0 drives, the followers replay its schedule);
 * each game is exactly the reference's ``run_simulation`` loop (round until
   ``game.game_over``) with a seeded ``ByzantineConsensusGame``;
 * rank 0 gathers every game's ``get_statistics()`` and writes one JSON: the
@@ -27,7 +29,6 @@ launch covers the whole sweep:
 import argparse
 import json
 import os
-import queue
 import random
 import sys
 import threading
@@ -99,47 +100,60 @@ def play_game(seed: int, honest: int, byzantine: int, max_rounds: int, value_ran
     return rec
 
 
-def run_games(seeds: List[int], args, llm=None, lockstep: bool = False, checkpoint=None) -> List[Dict]:
-    """Play `seeds` with up to `args.concurrency` games in flight (worker threads).
+class SeedQueue:
+    """Seeds handed out one at a time; shared by every DP replica of the node.
 
-    `checkpoint`: optional open text file; each finished game is appended as one JSON line.
+    Replicas pull the next seed index from an atomic counter in the process
+    group's TCPStore (``store.add``), so a replica that drew short games takes
+    more of them -- no replica idles at the tail while another still has a
+    static share to play.  Single process: a local counter.
+    """
+
+    def __init__(self, seeds: List[int], store=None, key: str = "bcg_sweep_next"):
+        self.seeds, self.store, self.key = list(seeds), store, key
+        self._lock = threading.Lock()
+        self._next = 0
+
+    def pop(self):
+        if self.store is not None:
+            i = int(self.store.add(self.key, 1)) - 1
+        else:
+            with self._lock:
+                i, self._next = self._next, self._next + 1
+        return self.seeds[i] if i < len(self.seeds) else None
+
+
+def run_games(seeds, args, llm=None, checkpoint=None) -> List[Dict]:
+    """Play seeds with up to `args.concurrency` games in flight (worker threads).
+
+    `seeds`: a list (played by this process alone) or a :class:`SeedQueue`
+    shared with the other replicas.  `checkpoint`: optional open text file;
+    each finished game is appended as one JSON line.
     """
     lo, hi = map(int, args.value_range.split("-"))
-    work: "queue.Queue[int]" = queue.Queue()
-    for s in seeds:
-        work.put(s)
+    q = seeds if isinstance(seeds, SeedQueue) else SeedQueue(seeds)
     results, errors = [], []
     ck_lock = threading.Lock()
-    n_workers = max(1, min(args.concurrency, len(seeds)))
+    n_workers = max(1, min(args.concurrency, len(q.seeds)))
 
     def worker(i):
-        th = threading.current_thread()
-        th._bcg_participant = lockstep
-        th._bcg_order_key = (i,)
+        threading.current_thread()._bcg_order_key = (i,)
         try:
             while True:
-                try:
-                    seed = work.get_nowait()
-                except queue.Empty:
+                seed = q.pop()
+                if seed is None:
                     return
                 rec = play_game(seed, args.honest, args.byzantine, args.rounds, (lo, hi),
                                 args.byzantine_awareness)
+                rec["finished_at"] = time.perf_counter()
                 results.append(rec)
                 if checkpoint is not None:
                     with ck_lock:
-                        checkpoint.write(json.dumps(rec) + "\n")
+                        checkpoint.write(json.dumps({k: v for k, v in rec.items() if k != "finished_at"}) + "\n")
                         checkpoint.flush()
         except BaseException as exc:
             errors.append(exc)
-        finally:
-            if lockstep:
-                llm.unregister_client()
 
-    if lockstep:
-        # TP ranks of a group play the same seeds in the same worker slots: the
-        # coalescer turns their calls into identical batches on every rank
-        for _ in range(n_workers):
-            llm.register_client()
     threads = [threading.Thread(target=worker, args=(i,)) for i in range(n_workers)]
     for t in threads:
         t.start()
@@ -217,17 +231,24 @@ def _main(args) -> Dict:
               quantization=C.VLLM_CONFIG.get("quantization"), seed=engine_seed)
     EngineAgent._shared_llm, EngineAgent._shared_model_name = llm, model
     EngineAgent._shared_model_config = dict(C.VLLM_CONFIG)
-    lockstep = args.tp > 1
-    if not lockstep:
-        llm.start_continuous_batching()
+    from .prompts import all_schemas
+    llm.precompile(all_schemas(lo, hi))  # every rank, same order (TP: identical FSM row bases)
 
+    ctrl = None
+    if lay.world > 1:
+        import torch.distributed as dist
+        # results / barriers on a CPU group: never queued behind the engine's HIP work
+        ctrl = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else None
     done = load_checkpoints(args.out) if args.resume else {}
     if lay.world > 1:  # every rank has read the checkpoints before anyone appends
-        import torch.distributed as dist
-        dist.barrier()
+        dist.barrier(group=ctrl)
     all_seeds = [args.seed0 + i for i in range(args.seeds)]
     todo = [s for s in all_seeds if s not in done]
-    seeds = [s for i, s in enumerate(todo) if i % dp == dp_rank]  # identical split on every rank
+    store = None
+    if lay.world > 1:
+        from torch.distributed.distributed_c10d import _get_default_store
+        store = _get_default_store()
+    queue_ = SeedQueue(todo, store, key=f"bcg_sweep_next_{args.seed0}_{len(todo)}")
     ck = None
     if lay.tp_rank == 0:
         os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
@@ -238,25 +259,40 @@ def _main(args) -> Dict:
         if torn:
             ck.write("\n")  # seal a torn last line so the next record parses
     t0 = time.perf_counter()
+    games = []
     try:
-        games = run_games(seeds, args, llm, lockstep, checkpoint=ck)
+        if llm.is_driver:  # the group's rank 0 plays; TP followers replay its schedule
+            llm.start_continuous_batching()
+            games = run_games(queue_, args, llm, checkpoint=ck)
+        else:
+            llm.serve_worker()
     finally:
         if ck is not None:
             ck.close()
+        if llm.is_driver:
+            llm.shutdown()  # releases the followers
     elapsed = time.perf_counter() - t0
-    mine = games if lay.tp_rank == 0 else []
+    busy = max((g["finished_at"] for g in games), default=t0 + elapsed) - t0
+    for g in games:
+        g.pop("finished_at", None)
 
     if lay.world > 1:
-        import torch.distributed as dist
         gathered = [None] * lay.world
-        dist.all_gather_object(gathered, {"games": mine, "elapsed": elapsed})
+        dist.all_gather_object(gathered, {"games": games, "elapsed": elapsed, "busy": busy,
+                                          "driver": llm.is_driver}, group=ctrl)
         games = sorted((g for part in gathered for g in part["games"]), key=lambda r: r["seed"])
         elapsed = max(part["elapsed"] for part in gathered)
+        drivers = [p for p in gathered if p["driver"]]
+        # idle tail: how long replicas waited for the slowest one after their last game
+        tail = [elapsed - p["busy"] for p in drivers]
+    else:
+        tail = [elapsed - busy]
     if done:
         resumed = [done[s] for s in all_seeds if s in done]
         games = sorted(games + resumed, key=lambda r: r["seed"])
     summary = summarize(games, elapsed, lay.world)
     summary["resumed_games"] = len(done)
+    summary["replica_idle_tail_frac"] = round(max(tail) / elapsed, 4) if elapsed > 0 else 0.0
     summary["config"] = {"model": model, "honest": args.honest, "byzantine": args.byzantine,
                          "max_rounds": args.rounds, "value_range": [lo, hi], "tp": args.tp, "dp": dp,
                          "byzantine_awareness": args.byzantine_awareness, "seed0": args.seed0,
@@ -268,7 +304,8 @@ def _main(args) -> Dict:
             json.dump(summary, fh, indent=2)
         brief = {k: v for k, v in summary.items() if k != "per_game"}
         print(json.dumps(brief), file=sys.__stdout__ if sys.stdout is sys.stderr else sys.stdout, flush=True)
-    llm.shutdown()
+    if not llm.is_driver:
+        llm.shutdown()
     EngineAgent._shared_llm = None
     destroy()
     return summary

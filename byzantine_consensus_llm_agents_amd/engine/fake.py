@@ -12,8 +12,10 @@ vote stop once every proposal shown this round is equal; Byzantine agents
 act pseudo-randomly (including abstentions).
 """
 
+import collections
 import hashlib
 import json
+import os
 import random
 import re
 from typing import Any, Dict, Optional
@@ -82,22 +84,101 @@ def scripted_text(prompt: str, schema: Optional[Dict], seed: int = 0) -> str:
     return json.dumps(scripted_object(prompt, schema, seed))
 
 
+# ------------------------------------------------------------ fault injection
+_AGENT_RE = re.compile(r"You are (agent_\d+)")
+_DECIDE_ROUND_RE = re.compile(r"=== ROUND (\d+) ===")
+_VOTE_ROUND_RE = re.compile(r"=== (?:VOTING PHASE|BYZANTINE VOTING) - Round (\d+)/")
+
+
+class InjectedEngineFault(RuntimeError):
+    """Raised by the scripted engine for a call that contains a prompt planned to crash it."""
+
+
+class FaultInjector:
+    """Deterministic engine failures for the retry-ladder parity goldens.
+
+    A plan is a list of rules ``{"agent": "agent_3", "round": 2, "phase":
+    "decide"|"vote", "tries": [1, 2], "mode": "invalid_json"|"short"|"exception"}``.
+    ``tries`` counts the requests of that (agent, round, phase) in the order
+    they are made -- batched attempts, then the sequential attempts (whose
+    prompts carry the ``RETRY ATTEMPT k/3`` suffix).  The reference and this
+    framework send every agent's requests in the same order, whatever the
+    batching, so the same plan fails the same requests on both sides:
+
+    * ``invalid_json`` -- unparsable text (batch and sequential validity fail);
+    * ``short``        -- parsable JSON that fails the batched validity rule
+      (internal strategy < 3 chars, reasoning < 10) but passes the sequential
+      one (non-empty fields); votes: an out-of-enum decision;
+    * ``exception``    -- the engine call raises (only meaningful where both
+      sides batch identically: homogeneous-schema configurations).
+    """
+
+    def __init__(self, plan):
+        self.plan = list(plan or [])
+        self.tries = collections.Counter()
+
+    @staticmethod
+    def identify(prompt: str, schema: Optional[Dict]):
+        agent = _AGENT_RE.search(prompt)
+        props = (schema or {}).get("properties", {})
+        if "decision" in props:
+            phase, rnd = "vote", _VOTE_ROUND_RE.search(prompt)
+        else:
+            phase, rnd = "decide", _DECIDE_ROUND_RE.search(prompt)
+        return (agent.group(1) if agent else None, int(rnd.group(1)) if rnd else None, phase)
+
+    def mode_for(self, prompt: str, schema: Optional[Dict]) -> Optional[str]:
+        """Count this request and return the planned failure mode (or None)."""
+        if not self.plan:
+            return None
+        key = self.identify(prompt, schema)
+        self.tries[key] += 1
+        t = self.tries[key]
+        for rule in self.plan:
+            if (rule["agent"], rule["round"], rule["phase"]) == key and t in rule["tries"]:
+                return rule["mode"]
+        return None
+
+    def answer_batch(self, prompts, schemas, seed: int = 0):
+        """Texts for one engine call; raises InjectedEngineFault if any prompt plans it."""
+        modes = [self.mode_for(p, s) for p, s in zip(prompts, schemas)]
+        if "exception" in modes:
+            raise InjectedEngineFault("injected engine fault")
+        out = []
+        for p, s, m in zip(prompts, schemas, modes):
+            if m == "invalid_json":
+                out.append("I cannot answer in JSON right now {")
+            elif m == "short":
+                is_vote = "decision" in (s or {}).get("properties", {})
+                out.append(json.dumps({"decision": "maybe"} if is_vote else
+                                      {"internal_strategy": "ok", "value": 7, "public_reasoning": "short"}))
+            else:
+                out.append(scripted_text(p, s, seed))
+        return out
+
+
 class FakeBackend:
     """Engine backend answering every request with :func:`scripted_text`."""
 
     name = "fake"
 
-    def __init__(self, seed: int = 0):
+    def __init__(self, seed: int = 0, faults=None):
         self.seed = seed
         self.calls = 0
+        self.delay_s = float(os.environ.get("BCG_FAKE_DELAY_S", "0") or 0)
+        if faults is None and os.environ.get("BCG_FAKE_FAULTS"):
+            faults = json.loads(os.environ["BCG_FAKE_FAULTS"])
+        self.faults = FaultInjector(faults) if faults else None
 
     def generate(self, prompts, params_list):
         self.calls += 1
-        texts = []
-        for prompt, params in zip(prompts, params_list):
-            schema = params.guided_decoding.json if params.guided_decoding is not None else None
-            texts.append(scripted_text(prompt, schema, self.seed))
-        return texts
+        if self.delay_s:  # simulated engine latency per call (load-balance tests)
+            import time
+            time.sleep(self.delay_s)
+        schemas = [p.guided_decoding.json if p.guided_decoding is not None else None for p in params_list]
+        if self.faults is not None:
+            return self.faults.answer_batch(prompts, schemas, self.seed)
+        return [scripted_text(p, s, self.seed) for p, s in zip(prompts, schemas)]
 
     def shutdown(self):
         pass

@@ -11,12 +11,19 @@ real Qwen tokenizer: ~4), which keeps prefill/decode shapes and the
 guided-decoding mask work representative.  Results produced with it are
 labelled "synthetic tokenizer" by the benchmark.
 
-The trained file is cached in ``<repo>/.cache/tokenizers``; concurrent
-processes serialise on a lock file so only one trains.
+Reproducibility: the trained files ship with the package
+(``engine/assets/synthetic-<family>-v1.json.gz``) and their SHA-256 is pinned
+below (``PINNED_SHA256``), so every box -- whatever its site-packages --
+tokenises identically.  Only when an asset is missing is the tokenizer
+re-trained from the image's text corpus (cached in ``<repo>/.cache/tokenizers``,
+concurrent processes serialise on a lock file); a re-trained file whose hash
+differs from the pin is refused unless ``BCG_ALLOW_UNPINNED_TOKENIZER=1``.
 """
 
 import fcntl
 import glob
+import gzip
+import hashlib
 import json
 import os
 from functools import lru_cache
@@ -26,6 +33,13 @@ from tokenizers import Regex, Tokenizer, decoders, models, pre_tokenizers, train
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CACHE_DIR = os.environ.get("BCG_TOKENIZER_CACHE", os.path.join(REPO, ".cache", "tokenizers"))
+ASSET_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets")
+
+# sha256 of the (uncompressed) synthetic tokenizer JSON every result was produced with
+PINNED_SHA256 = {
+    "qwen": "49bafd542f956b0e25607fa604a39aaaec17304fa3e7e507e1675ee4408f2ff2",
+    "mistral": "78a20091e6e5007467688e582b23fcaff114a5b879b108b29d4d2090eac6ce99",
+}
 
 QWEN_PATTERN = (r"(?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}| ?[^\s\p{L}\p{N}]+[\r\n]*"
                 r"|\s*[\r\n]+|\s+(?!\S)|\s+")
@@ -172,14 +186,34 @@ def load_tokenizer(model_name: str, model_dir: Optional[str] = None) -> BCGToken
             tok = BCGTokenizer(Tokenizer.from_file(path), eos, synthetic=False, name=path)
             _CACHE[key] = tok
             return tok
-    os.makedirs(CACHE_DIR, exist_ok=True)
-    path = os.path.join(CACHE_DIR, f"synthetic-{family}-v1.json")
-    if not os.path.exists(path):
-        with open(path + ".lock", "w") as lock:
-            fcntl.flock(lock, fcntl.LOCK_EX)
-            if not os.path.exists(path):
-                _train_synthetic(family, path)
-            fcntl.flock(lock, fcntl.LOCK_UN)
-    tok = BCGTokenizer(Tokenizer.from_file(path), eos, synthetic=True, name=f"synthetic-{family}")
+    tok = BCGTokenizer(Tokenizer.from_str(synthetic_json(family)), eos, synthetic=True,
+                       name=f"synthetic-{family}")
     _CACHE[key] = tok
     return tok
+
+
+def synthetic_json(family: str) -> str:
+    """The pinned synthetic tokenizer of `family` (shipped asset, else re-trained + verified)."""
+    asset = os.path.join(ASSET_DIR, f"synthetic-{family}-v1.json.gz")
+    if os.path.exists(asset):
+        with gzip.open(asset, "rb") as fh:
+            raw = fh.read()
+        source = asset
+    else:
+        os.makedirs(CACHE_DIR, exist_ok=True)
+        path = os.path.join(CACHE_DIR, f"synthetic-{family}-v1.json")
+        if not os.path.exists(path):
+            with open(path + ".lock", "w") as lock:
+                fcntl.flock(lock, fcntl.LOCK_EX)
+                if not os.path.exists(path):
+                    _train_synthetic(family, path)
+                fcntl.flock(lock, fcntl.LOCK_UN)
+        with open(path, "rb") as fh:
+            raw = fh.read()
+        source = path
+    digest = hashlib.sha256(raw).hexdigest()
+    if digest != PINNED_SHA256[family] and os.environ.get("BCG_ALLOW_UNPINNED_TOKENIZER") != "1":
+        raise RuntimeError(f"synthetic {family} tokenizer {source} has sha256 {digest}, pinned "
+                           f"{PINNED_SHA256[family]}: results would not be comparable "
+                           "(set BCG_ALLOW_UNPINNED_TOKENIZER=1 to use it anyway)")
+    return raw.decode("utf-8")

@@ -151,3 +151,17 @@ def test_engine_admission_batching_cpu(fresh_engine_state):
     llm.shutdown()
     assert not errors, errors[0]
     assert len(results) == 16 and set(results) <= {"stop", "continue"}
+
+
+def test_synthetic_tokenizer_is_pinned(monkeypatch):
+    """The shipped synthetic tokenizers match their pinned SHA-256 (same token ids on every
+    box, whatever its site-packages); a file with another hash is refused."""
+    import hashlib
+
+    from byzantine_consensus_llm_agents_amd.engine import tokenizer as T
+    for fam in ("qwen", "mistral"):
+        assert hashlib.sha256(T.synthetic_json(fam).encode()).hexdigest() == T.PINNED_SHA256[fam]
+    monkeypatch.setitem(T.PINNED_SHA256, "mistral", "0" * 64)
+    monkeypatch.delenv("BCG_ALLOW_UNPINNED_TOKENIZER", raising=False)
+    with pytest.raises(RuntimeError, match="pinned"):
+        T.synthetic_json("mistral")

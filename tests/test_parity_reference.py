@@ -30,6 +30,8 @@ def _run_ours(rec, tmp_path, cfg, monkeypatch):
         return orig(self, prompts, params)
 
     monkeypatch.setattr(fake_mod.FakeBackend, "generate", recording)
+    if rec.get("faults"):  # the same failure plan the reference ran under (tools/gen_golden.py)
+        monkeypatch.setenv("BCG_FAKE_FAULTS", json.dumps(rec["faults"]))
     monkeypatch.chdir(tmp_path)
     cfg.ENGINE_CONFIG["backend"] = "fake"
     cfg.BCG_CONFIG["value_range"] = tuple(rec["value_range"])
@@ -43,7 +45,19 @@ def _run_ours(rec, tmp_path, cfg, monkeypatch):
         results = json.load(fh)
     with open(os.path.join(tmp_path, "results", "metrics", "run_001.csv")) as fh:
         header = fh.read().splitlines()[0]
-    return sent, results, header
+    with open(os.path.join(tmp_path, "results", "logs", "run_001_log.txt")) as fh:
+        log = fh.read()
+    return sent, results, header, log
+
+
+def _sim_log_lines(text):
+    """The simulator's own log lines ("[LEVEL] ..."), in order, up to the end of the game;
+    agents' console lines are left out (our sequential retries run concurrently, so their
+    prints interleave), and so is the results display (the golden run bypasses the
+    reference's display_results crash with 0 Byzantine agents: tools/gen_golden.py)."""
+    lines = [ln for ln in text.splitlines() if ln.startswith("[") and "] " in ln[:12]]
+    end = next((i for i, ln in enumerate(lines) if ln.endswith("SIMULATION COMPLETE")), len(lines))
+    return lines[:end + 1]
 
 
 @pytest.mark.skipif(not GOLDEN, reason="no golden fixtures")
@@ -51,11 +65,18 @@ def _run_ours(rec, tmp_path, cfg, monkeypatch):
 def test_reference_parity(path, tmp_path, fresh_engine_state, monkeypatch):
     with open(path) as fh:
         rec = json.load(fh)
-    sent, results, header = _run_ours(rec, tmp_path, fresh_engine_state, monkeypatch)
+    sent, results, header, log = _run_ours(rec, tmp_path, fresh_engine_state, monkeypatch)
 
     ref_prompts = [(p, s, c["temperature"], c["max_tokens"])
                    for c in rec["engine_calls"] for p, s in zip(c["prompts"], c["schemas"])]
     assert len(sent) == len(ref_prompts)
+    if rec.get("faults"):
+        # sequential retries of several agents run concurrently here (one coalesced engine
+        # call per attempt), one agent after another in the reference: same requests,
+        # per-agent order preserved, global order may differ
+        key = lambda x: (x[0], json.dumps(x[1], sort_keys=True), x[2], x[3])  # noqa: E731
+        sent, ref_prompts = sorted(sent, key=key), sorted(ref_prompts, key=key)
+        assert _sim_log_lines(log) == _sim_log_lines(rec["log"])
     for i, (ours, ref) in enumerate(zip(sent, ref_prompts)):
         assert ours[0] == ref[0], f"prompt {i} differs"
         assert ours[1] == ref[1], f"schema {i} differs"
@@ -67,3 +88,17 @@ def test_reference_parity(path, tmp_path, fresh_engine_state, monkeypatch):
     assert header == rec["csv_header"]
     # one engine call per phase attempt on our side, never per prompt
     assert len(rec["engine_calls"]) >= sum(1 for _ in rec["engine_calls"] if _["n"] > 1)
+
+
+def test_fault_goldens_cover_every_retry_branch():
+    """The failure-injection goldens exercise each branch of the reference's retry ladder
+    (main.py:293-352 decide, :376-478 vote; vllm_agent.py:445-448 engine exception)."""
+    logs = "".join(json.load(open(p)).get("log") or "" for p in GOLDEN)
+    for marker in ("[SEQUENTIAL RETRY]",                          # <=30 % failed -> sequential
+                   "[RETRY 2/3] Retrying", "[RETRY 3/3] Retrying",  # >30 % failed -> re-batch
+                   "they will abstain",                            # decide: all attempts failed
+                   "defaulting to CONTINUE",                       # vote: all attempts failed
+                   "Invalid vote on attempt", "Invalid response on attempt"):
+        assert marker in logs, marker
+    plans = [r for p in GOLDEN for r in json.load(open(p)).get("faults", [])]
+    assert {r["mode"] for r in plans} == {"invalid_json", "short", "exception"}

@@ -61,3 +61,23 @@ def test_sweep_resume_from_checkpoints(tmp_path, fresh_engine_state):
     assert resumed["per_game"] == full["per_game"]
     assert resumed["outcomes"] == full["outcomes"]
     assert sweep.load_checkpoints(out).keys() == {g["seed"] for g in full["per_game"]}
+
+
+def _lb_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), BCG_FAKE_DELAY_S="0.004")
+    from byzantine_consensus_llm_agents_amd.bcg import sweep
+    sweep.main(["--seeds", "64", "--seed0", "100", "--honest", "3", "--byzantine", "1", "--rounds", "8",
+                "--engine", "fake", "--concurrency", "1", "--out", out])
+
+
+def test_sweep_dynamic_seed_queue_balances_replicas(tmp_path):
+    """Uneven game lengths (1-8 rounds): replicas pull seeds from a shared counter,
+    every seed is played exactly once, and no replica idles long at the tail."""
+    out = str(tmp_path / "lb.json")
+    mp.start_processes(_lb_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    res = json.load(open(out))
+    assert [g["seed"] for g in res["per_game"]] == list(range(100, 164))
+    rounds = [g["total_rounds"] for g in res["per_game"]]
+    assert max(rounds) > min(rounds)  # the games really are uneven
+    assert res["replica_idle_tail_frac"] < 0.05, res["replica_idle_tail_frac"]

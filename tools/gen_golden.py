@@ -23,13 +23,38 @@ import types
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 
+def _r(agent, rnd, phase, tries, mode):
+    return {"agent": agent, "round": rnd, "phase": phase, "tries": tries, "mode": mode}
+
+
+# Retry-ladder failure paths (reference main.py:293-352 decide, :376-478 vote,
+# vllm_agent.py:445-448 engine exception), injected deterministically
+# (engine/fake.py FaultInjector) into the SAME scripted engine on both sides.
+FAULTS_H8B2 = [
+    _r("agent_1", 1, "decide", [1, 2], "invalid_json"),        # <=30 % -> sequential, succeeds on its 2nd try
+    _r("agent_4", 1, "decide", [1, 2, 3, 4], "invalid_json"),  # sequential: all 3 fail -> abstains
+    *[_r(f"agent_{i}", 2, "decide", [1], "short") for i in (0, 2, 5, 7)],  # 40 % -> re-batch
+    _r("agent_9", 3, "decide", [1, 2], "short"),               # batch-invalid, sequential-valid answer
+    _r("agent_3", 1, "vote", [1, 2, 3, 4], "invalid_json"),    # sequential vote: all fail
+    *[_r(f"agent_{i}", 2, "vote", [1], "short") for i in (1, 6, 8, 9)],  # 40 % -> re-batch
+    _r("agent_2", 3, "vote", [1], "short"),                    # <=30 % -> sequential, succeeds
+    *[_r(f"agent_{i}", 4, "vote", [1, 2, 3], "invalid_json") for i in (0, 3, 5, 8)],  # 40 % x3 -> default continue
+]
+FAULTS_H4B0 = [
+    _r("agent_0", 1, "decide", [1], "exception"),              # engine raises -> {"error"} for all -> re-batch
+    _r("agent_1", 1, "vote", [1, 2, 3], "exception"),          # every batched vote attempt raises -> default continue
+    _r("agent_2", 2, "decide", [1, 2, 3], "exception"),        # every decide attempt raises -> all abstain
+]
+
 CONFIGS = [
-    # name, honest, byzantine, max_rounds, seed, awareness, value_range
+    # name, honest, byzantine, max_rounds, seed, awareness, value_range[, fault plan]
     ("h4b0", 4, 0, 5, 11, "may_exist", (0, 50)),
     ("h4b1", 4, 1, 6, 5, "may_exist", (0, 50)),
     ("h8b2", 8, 2, 4, 7, "may_exist", (0, 50)),
     ("h5b0_none", 5, 0, 4, 3, "none_exist", (10, 20)),
     ("h3b2", 3, 2, 5, 2, "may_exist", (0, 9)),
+    ("h8b2_faults", 8, 2, 4, 7, "may_exist", (0, 50), FAULTS_H8B2),
+    ("h4b0_exceptions", 4, 0, 6, 11, "may_exist", (0, 50), FAULTS_H4B0),
 ]
 
 
@@ -41,8 +66,9 @@ def load_fake():
     return mod
 
 
-def install_stub_vllm(log):
+def install_stub_vllm(log, faults=None):
     fake = load_fake()
+    injector = fake.FaultInjector(faults) if faults else None
     vllm = types.ModuleType("vllm")
     sp = types.ModuleType("vllm.sampling_params")
 
@@ -65,12 +91,12 @@ def install_stub_vllm(log):
         def generate(self, prompts, params):
             schema = params.guided_decoding.json if params.guided_decoding else None
             log.append({"n": len(prompts), "temperature": params.temperature, "max_tokens": params.max_tokens})
-            outs = []
             for p in prompts:
                 log[-1].setdefault("prompts", []).append(p)
                 log[-1].setdefault("schemas", []).append(schema)
-                outs.append(_Out(fake.scripted_text(p, schema, 0)))
-            return outs
+            if injector is not None:
+                return [_Out(t) for t in injector.answer_batch(prompts, [schema] * len(prompts), 0)]
+            return [_Out(fake.scripted_text(p, schema, 0)) for p in prompts]
 
     vllm.LLM, vllm.SamplingParams = LLM, SamplingParams
     sp.GuidedDecodingParams = GuidedDecodingParams
@@ -79,9 +105,9 @@ def install_stub_vllm(log):
     sys.modules["vllm.sampling_params"] = sp
 
 
-def run_reference(ref_dir, name, honest, byz, rounds, seed, awareness, vr):
+def run_reference(ref_dir, name, honest, byz, rounds, seed, awareness, vr, faults=None):
     log = []
-    install_stub_vllm(log)
+    install_stub_vllm(log, faults)
     src = os.path.join(ref_dir, "byzantine_consensus_game")
     for m in ["config", "main", "byzantine_consensus", "a2a_sim", "agent_network",
               "communication_protocol", "protocol_factory", "bcg_agents", "vllm_agent"]:
@@ -115,6 +141,8 @@ def run_reference(ref_dir, name, honest, byz, rounds, seed, awareness, vr):
             results = json.load(fh)
         with open(os.path.join("results", "metrics", "run_001.csv")) as fh:
             csv_text = fh.read()
+        with open(os.path.join("results", "logs", "run_001_log.txt")) as fh:
+            log_text = fh.read() if faults else None
     finally:
         os.chdir(cwd)
         sys.path.remove(src)
@@ -125,7 +153,7 @@ def run_reference(ref_dir, name, honest, byz, rounds, seed, awareness, vr):
     csv_lines = csv_text.splitlines()
     return {"name": name, "honest": honest, "byzantine": byz, "rounds": rounds, "seed": seed,
             "awareness": awareness, "value_range": list(vr), "engine_calls": log,
-            "results": results, "csv_header": csv_lines[0]}
+            "results": results, "csv_header": csv_lines[0], "faults": faults or [], "log": log_text}
 
 
 def main():
