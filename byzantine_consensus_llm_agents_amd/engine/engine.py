@@ -145,7 +145,7 @@ class InferenceEngine:
         self.args = args
         self.timer = PhaseTimer()
         self.stats = {"prompt_tokens": 0, "cached_tokens": 0, "generated_tokens": 0,
-                      "decode_steps": 0, "prefill_chunks": 0, "calls": 0}
+                      "decode_steps": 0, "decode_row_steps": 0, "prefill_chunks": 0, "calls": 0}
         cfg = args.model_cfg
         self.backend = args.backend
         if self.backend == "hip" and not torch.cuda.is_available():
@@ -670,6 +670,9 @@ class InferenceEngine:
         with self.timer.phase("decode"):
             steps = self.graphs.run_burst(n) if self.graphs is not None else self._eager_burst(n)
         self.stats["decode_steps"] += steps
+        self.stats["decode_row_steps"] += steps * len(rows)  # mean live rows = this / decode_steps
+        band = f"rows_le_{min(768, 1 << max(0, (n - 1).bit_length()))}"
+        self.stats[band] = self.stats.get(band, 0) + steps
         self._bursts += 1
 
     def _eager_burst(self, n: int) -> int:

@@ -255,6 +255,8 @@ class DecoderModel:
     def forward(self, tokens: torch.Tensor, meta: AttnMeta, k_cache: torch.Tensor,
                 v_cache: torch.Tensor) -> torch.Tensor:
         """Returns logits ``[len(logits_idx) or B, vocab]`` (full vocab, fp32 or bf16)."""
+        if self.quant is None and self.tp.size == 1 and hasattr(self.ops, "linear_residual"):
+            return self._forward_fused(tokens, meta, k_cache, v_cache)
         ops, c = self.ops, self.cfg
         fp8 = self.quant == "fp8"
         residual = None
@@ -297,3 +299,41 @@ class DecoderModel:
         h, _ = ops.add_rmsnorm(x, residual, self.final_norm, c.rms_eps)
         logits = ops.linear(h, self.lm_head)
         return self.tp.all_gather_last(logits)
+
+    def _forward_fused(self, tokens, meta, k_cache, v_cache):
+        """TP=1 bf16 forward with the GEMM epilogues fused (hand MFMA kernel where the
+        GEMM plan picks it, ops/gemm_plan.py):
+
+            o_proj   : residual <- residual + attn Wo^T       (+ plain RMSNorm after)
+            gate_up  : h <- silu(x Wg^T) * (x Wu^T)           (K-ACT inside the GEMM)
+            down     : residual <- residual + h Wd^T          (+ plain RMSNorm of the next layer)
+
+        so the residual stream never takes a separate add pass and the [T, 2I]
+        gate_up activation is never written to HBM.
+        """
+        ops, c = self.ops, self.cfg
+        residual = None
+        for li, L in enumerate(self.layers):
+            if li == 0:  # embedding gather fused with the first input norm
+                h, residual = ops.embed_rmsnorm(tokens, self.embed, L["ln1"], c.rms_eps)
+            else:
+                h = ops.rmsnorm(residual, L["ln1"], c.rms_eps)
+            qkv = ops.linear(h, L["qkv"], L.get("qkv_bias"))
+            q = ops.qk_norm_rope_kv_write(qkv, meta.positions, meta.slots, self.n_q, self.n_kv, self.hd,
+                                          L.get("q_norm"), L.get("k_norm"), c.rms_eps, self.cos_sin,
+                                          k_cache, v_cache, li)
+            if meta.decode:
+                attn = ops.paged_attention_decode(q, k_cache, v_cache, li, meta.block_tables,
+                                                  meta.seq_lens, self.scale, meta.workspace)
+            else:
+                attn = ops.paged_attention_prefill(q, k_cache, v_cache, li, meta.block_tables,
+                                                   meta.q_start, meta.seq_lens, self.scale, meta.max_q_len,
+                                                   meta.tiles)
+            residual = ops.linear_residual(attn, L["o"], residual)
+            h = ops.rmsnorm(residual, L["ln2"], c.rms_eps)
+            act = ops.linear_silu(h, L["gate_up"])
+            residual = ops.linear_residual(act, L["down"], residual)
+        if meta.logits_idx is not None:
+            residual = residual.index_select(0, meta.logits_idx)
+        h = ops.rmsnorm(residual, self.final_norm, c.rms_eps)
+        return ops.linear(h, self.lm_head)

@@ -31,6 +31,8 @@ def _torch_ops() -> SimpleNamespace:
         paged_attention_decode=decode,
         paged_attention_prefill=prefill,
         silu_mul=_ref.silu_mul,
+        linear_silu=_ref.linear_silu,
+        linear_residual=_ref.linear_residual,
         sample_step=_ref.sample_step,
         quant_fp8=_ref.quant_fp8,
         add_rmsnorm_fp8=_ref.add_rmsnorm_fp8,

@@ -1,0 +1,79 @@
+"""Which GEMM runs where: the hand MFMA kernel (csrc/kernels/gemm.hip) or hipBLASLt.
+
+Decode projections are skinny (M = live rows of a decode bucket, 1..768) and
+the hand kernel's tile shapes, fused epilogues and XCD-aware order are built
+for them; prefill chunks (M = 16384) stay on hipBLASLt's tuned kernels.  The
+choice per (M, N, K, epilogue) comes from a table measured on the GPU
+(``tools/tune_hand_gemm.py`` -> ``engine/tuned/hand_gemm.json``: for every
+decode bucket and projection shape, every tile configuration and the library
+are timed and the fastest is kept).  Shapes the table does not cover use a
+simple rule (hand kernel up to ``max_m`` rows).
+
+``BCG_HAND_GEMM``: ``0`` = library only, ``1`` (default) = table / rule,
+``force`` = hand kernel wherever the shape is supported (tests).
+"""
+
+import ctypes
+import json
+import os
+from typing import Dict, Optional, Tuple
+
+TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "engine", "tuned",
+                     "hand_gemm.json")
+TILES = ((128, 128), (64, 128), (128, 64), (256, 128), (64, 256), (64, 64), (32, 128),  # csrc/kernels/gemm.hip CFGS
+         (256, 128), (128, 256), (128, 128))
+N_CFGS = len(TILES)
+SPLITS = (1, 2, 3, 4, 6, 8)
+
+
+class GemmPlan:
+    def __init__(self, lib=None, table: Optional[str] = TABLE, max_m: int = 1024):
+        self.mode = os.environ.get("BCG_HAND_GEMM", "1")
+        self.max_m = max_m
+        self.tiles = {}
+        for cfg in range(N_CFGS):
+            self.tiles[cfg] = TILES[cfg]
+            if lib is not None:  # the library is the source of truth
+                bm, bn = ctypes.c_int(), ctypes.c_int()
+                if lib.bcg_gemm_tile(cfg, ctypes.byref(bm), ctypes.byref(bn)) == 0:
+                    self.tiles[cfg] = (bm.value, bn.value)
+        self.table: Dict[Tuple[int, int, int, int], Tuple[int, int]] = {}
+        if table and os.path.exists(table):
+            with open(table) as fh:
+                for key, choice in json.load(fh).get("choice", {}).items():
+                    m, n, k, e = map(int, key.split(","))
+                    self.table[(m, n, k, e)] = tuple(choice) if isinstance(choice, list) else (int(choice), 1)
+
+    def supported(self, cfg: int, M: int, N: int, K: int, epi: int, split_k: int = 1) -> bool:
+        if cfg not in self.tiles or M <= 0 or K % 64 or K <= 0 or split_k < 1 or K // 64 < split_k:
+            return False
+        bn = self.tiles[cfg][1]
+        if N % bn:
+            return False
+        if epi == 1 and (N % 2 or (N // 2) % (bn // 2)):
+            return False
+        return True
+
+    def default_cfg(self, M: int) -> int:
+        return 1 if M <= 64 else 0
+
+    def choose(self, M: int, N: int, K: int, epi: int) -> Optional[Tuple[int, int]]:
+        """(tile configuration, split-K) of the hand kernel, or None for the library path."""
+        if self.mode == "0":
+            return None
+        if self.mode == "force":
+            for cfg in (self.default_cfg(M),) + tuple(range(N_CFGS)):
+                if self.supported(cfg, M, N, K, epi):
+                    return (cfg, 1)
+            return None
+        choice = self.table.get((M, N, K, epi))
+        if choice is None and self.table:  # nearest measured M above (same projection shape)
+            above = [m for (m, n, k, e) in self.table if (n, k, e) == (N, K, epi) and m >= M]
+            if above:
+                choice = self.table[(min(above), N, K, epi)]
+        if choice is not None:
+            return choice if choice[0] >= 0 and self.supported(choice[0], M, N, K, epi, choice[1]) else None
+        if M > self.max_m or self.table:  # a measured table exists: unlisted shapes stay on the library
+            return None
+        cfg = self.default_cfg(M)
+        return (cfg, 1) if self.supported(cfg, M, N, K, epi) else None

@@ -52,6 +52,10 @@ def load_library(path: str = None) -> ctypes.CDLL:
         "bcg_add_rmsnorm_fp8": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_int,
                                 c_void_p],
         "bcg_silu_mul_fp8": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+        "bcg_gemm_nt": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                        c_int, c_int, c_int, c_int, c_int, c_void_p],
+        "bcg_gemm_tile": [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)],
+        "bcg_gemm_num_cfgs": [],
         "bcg_guided_sample": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                               c_uint32, c_int, c_int, c_int, c_int, c_void_p],
@@ -119,7 +123,12 @@ def hip_ops() -> SimpleNamespace:
         return out, residual
 
     def rmsnorm(x, w, eps):
-        out, _ = add_rmsnorm(x, None, w, eps)
+        """Plain RMSNorm (mode 2: the residual stream is not touched)."""
+        _req(x.dtype == torch.bfloat16 and x.is_contiguous() and x.dim() == 2, "rmsnorm: x bf16 [T,H]")
+        T, H = x.shape
+        _req(w.shape == (H,) and w.dtype == torch.bfloat16, "rmsnorm: weight [H] bf16")
+        out = torch.empty_like(x)
+        _check(lib.bcg_add_rmsnorm(_p(x), None, _p(w), _p(out), T, H, eps, 2, _stream()), "rmsnorm")
         return out
 
     def silu_mul(gu):
@@ -215,9 +224,14 @@ def hip_ops() -> SimpleNamespace:
         return max(1, min(512 // nblocks, ksteps // 8))
 
     def linear(x, w, bias=None):
-        """y = x W^T (+b): MFMA weight-streaming kernel for decode shapes, hipBLASLt otherwise."""
+        """y = x W^T (+b): hand MFMA GEMM where the plan says it beats hipBLASLt (decode
+        shapes), the optional skinny weight-streaming kernel, hipBLASLt otherwise."""
         M, K = x.shape
         N = w.shape[0]
+        if x.is_contiguous() and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
+            cfg = plan.choose(M, N, K, 0)
+            if cfg is not None:
+                return gemm_nt(x, w, cfg, 0, bias=bias)
         if not (use_skinny and M <= skinny_max_m and N % 128 == 0 and K % 128 == 0 and x.is_contiguous()
                 and w.is_contiguous() and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
             return torch.nn.functional.linear(x, w, bias)
@@ -228,6 +242,69 @@ def hip_ops() -> SimpleNamespace:
         _check(lib.bcg_gemm_skinny(_p(x), _p(w), _p(bias) if bias is not None else None, _p(y),
                                    _p(ws) if ws is not None else None, M, N, K, split, _stream()), "gemm_skinny")
         return y
+
+    from .gemm_plan import GemmPlan
+    plan = GemmPlan(lib)
+
+    counters = {}  # per (device, stream): split-K arrival counters, zero between launches
+
+    def _counters(dev):
+        key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+        if key not in counters:
+            counters[key] = torch.zeros(1 << 16, dtype=torch.int32, device=dev)
+        return counters[key]
+
+    def gemm_nt(x, w, cfg, epi=0, bias=None, residual=None, out=None, split_k=1):
+        """Hand MFMA GEMM (csrc/kernels/gemm.hip): x [M,K] @ w[N,K]^T with epilogue `epi`
+        (0 store(+bias), 1 silu(gate)*up -> [M, N/2], 2 residual + acc); `split_k` K-slices
+        reduced in the kernel by the last-arriving workgroup of each tile."""
+        if isinstance(cfg, (tuple, list)):
+            cfg, split_k = cfg
+        M, K = x.shape
+        N = w.shape[0]
+        _req(x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()
+             and w.shape[1] == K, "gemm_nt: contiguous bf16 x [M,K], w [N,K]")
+        _req(plan.supported(cfg, M, N, K, epi, split_k),
+             f"gemm_nt: shape {M}x{N}x{K} epi {epi} split {split_k} unsupported by tile {cfg}")
+        width = N // 2 if epi == 1 else N
+        if out is None:
+            out = torch.empty(M, width, dtype=x.dtype, device=x.device)
+        _req(out.shape == (M, width) and out.is_contiguous() and out.dtype == torch.bfloat16, "gemm_nt: out")
+        if bias is not None:
+            _req(bias.shape == (N,) and bias.dtype == torch.bfloat16 and bias.is_contiguous(), "gemm_nt: bias")
+        if epi == 2:
+            _req(residual is not None and residual.shape == (M, N) and residual.is_contiguous()
+                 and residual.dtype == torch.bfloat16, "gemm_nt: residual [M,N] bf16")
+        ws = cnt = None
+        if split_k > 1:
+            bm, bn = plan.tiles[cfg]
+            tiles = (M + bm - 1) // bm * (N // bn)
+            _req(tiles <= (1 << 16), "gemm_nt: too many output tiles for split-K")
+            ws = torch.empty(tiles * split_k * bm * bn, dtype=torch.float32, device=x.device)
+            cnt = _counters(x.device)
+        _check(lib.bcg_gemm_nt(cfg, epi, _p(x), _p(w), _p(bias) if bias is not None else None,
+                               _p(residual) if residual is not None else None, _p(out),
+                               _p(ws) if ws is not None else None, _p(cnt) if cnt is not None else None,
+                               M, N, K, N // 2, split_k, _stream()), "gemm_nt")
+        return out
+
+    def linear_silu(x, w):
+        """silu(x Wg^T) * (x Wu^T), W = [gate; up] -- K-ACT fused into the gate_up GEMM."""
+        M, K = x.shape
+        cfg = plan.choose(M, w.shape[0], K, 1) if x.is_contiguous() and x.dtype == torch.bfloat16 else None
+        if cfg is None:
+            return silu_mul(linear(x, w))
+        return gemm_nt(x, w, cfg, 1)
+
+    def linear_residual(x, w, residual):
+        """residual <- residual + x W^T (in place; the o/down projection fused with the
+        residual-stream update of the next add+RMSNorm).  Returns `residual`."""
+        M, K = x.shape
+        cfg = plan.choose(M, w.shape[0], K, 2) if x.is_contiguous() and x.dtype == torch.bfloat16 else None
+        if cfg is None:
+            residual.add_(linear(x, w))
+            return residual
+        return gemm_nt(x, w, cfg, 2, residual=residual, out=residual)
 
     def sample_step(logits, fsm_next, fsm_dist, fsm_base, fsm_state, gen_count, max_new, temperature,
                     row_keys, done, seq_lens, out_tokens, next_tokens, seed, budget_aware, n_text_tokens,
@@ -287,7 +364,8 @@ def hip_ops() -> SimpleNamespace:
         return torch._scaled_mm(xq, wq.t(), scale_a=xs.view(-1, 1), scale_b=ws.view(1, -1), bias=bias,
                                 out_dtype=out_dtype)
 
-    return SimpleNamespace(name="hip", linear=linear, quant_fp8=quant_fp8, add_rmsnorm_fp8=add_rmsnorm_fp8,
+    return SimpleNamespace(name="hip", linear=linear, linear_silu=linear_silu, linear_residual=linear_residual,
+                           gemm_nt=gemm_nt, gemm_plan=plan, quant_fp8=quant_fp8, add_rmsnorm_fp8=add_rmsnorm_fp8,
                            silu_mul_fp8=silu_mul_fp8, linear_fp8=linear_fp8, rmsnorm=rmsnorm, add_rmsnorm=add_rmsnorm, silu_mul=silu_mul,
                            embed_rmsnorm=embed_rmsnorm,
                            qk_norm_rope_kv_write=qk_norm_rope_kv_write,

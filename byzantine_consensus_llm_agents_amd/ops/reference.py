@@ -129,6 +129,19 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     return out.reshape(T, n_q * hd).to(q.dtype)
 
 
+def linear_silu(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """silu(x Wg^T) * (x Wu^T) with W = [gate; up]: the fused gate_up GEMM epilogue (fp32 math)."""
+    gu = x.float() @ w.float().t()
+    inter = gu.shape[-1] // 2
+    return (torch.nn.functional.silu(gu[:, :inter]) * gu[:, inter:]).to(x.dtype)
+
+
+def linear_residual(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor) -> torch.Tensor:
+    """residual <- residual + x W^T, rounded once (the fused o/down GEMM epilogue); in place."""
+    residual.copy_((residual.float() + x.float() @ w.float().t()).to(residual.dtype))
+    return residual
+
+
 def silu_mul(gu: torch.Tensor) -> torch.Tensor:
     inter = gu.shape[-1] // 2
     g, u = gu[..., :inter].float(), gu[..., inter:].float()

@@ -34,18 +34,20 @@ __global__ __launch_bounds__(NORM_THREADS) void add_rmsnorm_kernel(
     if (vi < nvec) {
       u16x8 xv = *reinterpret_cast<const u16x8*>(x + base + vi * 8);
       u16x8 rv;
-      if (has_residual) rv = *reinterpret_cast<const u16x8*>(residual + base + vi * 8);
+      if (has_residual == 1) rv = *reinterpret_cast<const u16x8*>(residual + base + vi * 8);
       u16x8 nr;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float f = bf2f(xv[j]);
-        if (has_residual) f += bf2f(rv[j]);
+        if (has_residual == 1) f += bf2f(rv[j]);
         nr[j] = f2bf(f);
         f = bf2f(nr[j]);  // normalise the value actually stored (matches the reference)
         v[c][j] = f;
         ss += f * f;
       }
-      *reinterpret_cast<u16x8*>(residual + base + vi * 8) = nr;
+      // mode 2 = plain RMSNorm of x (the residual stream was already updated by the
+      // GEMM epilogue that produced x): nothing to write back
+      if (has_residual != 2) *reinterpret_cast<u16x8*>(residual + base + vi * 8) = nr;
     }
   }
   __shared__ float partial[NORM_THREADS / WAVE];

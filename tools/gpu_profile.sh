@@ -5,7 +5,7 @@ mkdir -p gpurun_out/prof
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
-  python bench.py --steps ${STEPS:-1} --warmup 0 --sims-per-gpu ${SIMS:-4} ${EXTRA} > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err
+  python bench.py --steps ${STEPS:-6} --warmup ${WARMUP:-4} --sims-per-gpu ${SIMS:-128} ${EXTRA} > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err
 rc=$?
 tail -3 gpurun_out/prof_bench.err
 cat gpurun_out/prof_bench.json
