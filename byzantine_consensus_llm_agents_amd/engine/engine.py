@@ -308,7 +308,8 @@ class InferenceEngine:
         self.slots: List[Optional[_Request]] = [None] * cap
         # one split-K scratch for every decode graph (they never run concurrently)
         ws = self._decode_ws_bytes() // 4
-        self.decode_ws = torch.empty(ws, dtype=torch.float32, device=dev) if ws else None
+        # zeros: the tail holds the decode kernel's split arrival counters (self-resetting)
+        self.decode_ws = torch.zeros(ws, dtype=torch.float32, device=dev) if ws else None
 
     def _phys(self, blocks: List[int]) -> List[int]:
         return [b + 1 for b in blocks]  # manager ids are shifted past scratch block 0

@@ -155,6 +155,7 @@ def hip_ops() -> SimpleNamespace:
         return q
 
     def decode_workspace_numel(B, n_q, hd, max_blocks, block_size=16):
+        """fp32 split partials (o, m, l) of the flash-decoding split-K."""
         split = lib.bcg_decode_split_tokens(B, 0, max_blocks * block_size)
         max_splits = (max_blocks * block_size + split - 1) // split
         return B * n_q * max_splits * (hd + 2)

@@ -204,49 +204,47 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt_kernel(
   }
 
   // ---- split-K: partial tiles -> workspace; the last-arriving split reduces ----
-  // (cdna_hip_programming.md "Projection GEMM at M = 256" item 2: plain stores,
-  //  vmcnt(0), barrier, agent-scope release, counter; acquire in the reducer)
+  // Hand-off without L2 maintenance (cdna_hip_programming.md §6 Guideline 16, R1):
+  // partials are stored WRITE-THROUGH (sc1), every wave drains vmcnt, barrier, one
+  // relaxed agent-scope ticket; the reducer reads the other slabs with sc1 loads.  (An
+  // agent-scope release/acquire pair is buffer_wbl2 + buffer_inv on gfx950: an L2
+  // write-back per episode.)
   if (split_k > 1) {
+    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
     float* slab = ws + static_cast<size_t>(tile) * split_k * (BM * BN);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(slab, 0, split_k * BM * BN * 4, 0x00020000);
     const int tid = threadIdx.x;
     __syncthreads();  // every wave is past its last ds_read: smem is reusable as the flag slot
     int* flag = reinterpret_cast<int*>(smem);
-    // element (i, j, e) of this lane lives at [split][(wave*NT*MT + i*MT + j)*256 + e*64 + lane]
-    float* mine = slab + static_cast<size_t>(split) * (BM * BN);
-    if (tid == 0) flag[0] = 0;
-    {
+    // block (i, j) of this wave: 256 floats, lane-major (4 per lane = one 16-B access)
 #pragma unroll
-      for (int i = 0; i < NT; ++i)
+    for (int i = 0; i < NT; ++i)
 #pragma unroll
-        for (int j = 0; j < MT; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) mine[((wave * NT + i) * MT + j) * 256 + e * 64 + lane] = acc[i][j][e];
-    }
+      for (int j = 0; j < MT; ++j) {
+        const int off = (split * (BM * BN) + ((wave * NT + i) * MT + j) * 256 + lane * 4) * 4;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, acc[i][j]), rs, off, 0, 16 /*sc1*/);
+      }
     vm_wait<0>();
     __syncthreads();
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      vm_wait<0>();
       const int prev = __hip_atomic_fetch_add(&counters[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = prev == split_k - 1;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        vm_wait<0>();
-        __hip_atomic_store(&counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-      }
+      if (last) __hip_atomic_store(&counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
       flag[0] = last;
     }
     __syncthreads();
     if (!flag[0]) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below
     for (int sp = 0; sp < split_k; ++sp) {
       if (sp == split) continue;
-      const float* other = slab + static_cast<size_t>(sp) * (BM * BN);
 #pragma unroll
       for (int i = 0; i < NT; ++i)
 #pragma unroll
-        for (int j = 0; j < MT; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[i][j][e] += other[((wave * NT + i) * MT + j) * 256 + e * 64 + lane];
+        for (int j = 0; j < MT; ++j) {
+          const int off = (sp * (BM * BN) + ((wave * NT + i) * MT + j) * 256 + lane * 4) * 4;
+          acc[i][j] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16 /*sc1*/));
+        }
     }
   }
 

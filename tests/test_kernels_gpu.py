@@ -101,6 +101,27 @@ def test_paged_attention_decode(hip, n_q, n_kv, hd, kv_dtype):
     _close(out, ref, atol=2e-2)
 
 
+def test_paged_attention_decode_shared_workspace_buckets(hip):
+    """One split-K workspace shared by launches of different batch sizes -- larger then
+    smaller, repeatedly, as the decode graphs of every bucket share it -- gives the
+    reference result every time."""
+    gen = torch.Generator().manual_seed(5)
+    n_q, n_kv, hd, NB = 40, 8, 128, 512
+    k, v = _caches(2, NB, n_kv, hd)
+    max_blocks = 128
+    ws = torch.zeros(hip.decode_workspace_numel(64, n_q, hd, max_blocks), dtype=torch.float32, device="cuda")
+    for B in (64, 16, 48, 8, 64, 33):
+        lens = torch.randint(1, 2000, (B,), generator=gen).tolist()
+        tables = torch.randint(1, NB, (B, max_blocks), generator=gen, dtype=torch.int32).cuda()  # blocks may repeat
+        seq = torch.tensor(lens, dtype=torch.int32, device="cuda")
+        q = torch.randn(B, n_q, hd, device="cuda", dtype=torch.bfloat16)
+        ref = R.paged_attention(q, k, v, 0, tables, torch.arange(B + 1, dtype=torch.int32, device="cuda"), seq,
+                                hd ** -0.5)
+        for _ in range(2):
+            out = hip.paged_attention_decode(q, k, v, 0, tables, seq, hd ** -0.5, ws)
+            _close(out, ref, atol=2e-2)
+
+
 def _prefill_tiles(q_start, seq_lens):
     tiles = []
     for i in range(len(q_start) - 1):
