@@ -61,11 +61,32 @@ class TPGroup:
                 torch.distributed.all_reduce(x, group=self.group)
         return x
 
+    def all_reduce_add_rmsnorm(self, x: torch.Tensor, residual: Optional[torch.Tensor], w: torch.Tensor,
+                               eps: float, ops):
+        """(rmsnorm(residual + sum_ranks x) * w, updated residual): the row-parallel projection's
+        all-reduce fused with the next residual add + RMSNorm where the xGMI kernel takes it."""
+        if (self.size > 1 and residual is not None and self.custom is not None
+                and self.custom.can_addnorm(x) and x.is_cuda):
+            return self.custom.all_reduce_add_rmsnorm(x, residual, w, eps), residual
+        return ops.add_rmsnorm(self.all_reduce_(x), residual, w, eps)
+
     def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
         if self.size == 1:
             return x
+        x = x.contiguous()
+        full_shape = x.shape[:-1] + (x.shape[-1] * self.size,)
+        if self.custom is not None and x.is_cuda and x.dtype == torch.bfloat16:
+            # small gathers (decode logits of a few rows) over the xGMI kernel: every rank
+            # places its shard in a zeroed full-width tensor and the shards are summed --
+            # exact (x + 0), graph-capturable, no RCCL call inside a captured decode step
+            full = torch.zeros(full_shape, dtype=x.dtype, device=x.device)
+            if self.custom.can(full):
+                w_ = x.shape[-1]
+                full[..., self.rank * w_:(self.rank + 1) * w_].copy_(x)
+                self.custom.all_reduce_(full)
+                return full
         parts = [torch.empty_like(x) for _ in range(self.size)]
-        torch.distributed.all_gather(parts, x.contiguous(), group=self.group)
+        torch.distributed.all_gather(parts, x, group=self.group)
         return torch.cat(parts, dim=-1)
 
 
@@ -268,8 +289,8 @@ class DecoderModel:
             else:
                 if li == 0:  # embedding gather fused with the first input norm
                     h, residual = ops.embed_rmsnorm(tokens, self.embed, L["ln1"], c.rms_eps)
-                else:
-                    h, residual = ops.add_rmsnorm(x, residual, L["ln1"], c.rms_eps)
+                else:  # x: this rank's partial down_proj output of the previous layer
+                    h, residual = self.tp.all_reduce_add_rmsnorm(x, residual, L["ln1"], c.rms_eps, ops)
                 qkv = ops.linear(h, L["qkv"], L.get("qkv_bias"))
             q = ops.qk_norm_rope_kv_write(qkv, meta.positions, meta.slots, self.n_q, self.n_kv, self.hd,
                                           L.get("q_norm"), L.get("k_norm"), c.rms_eps, self.cos_sin,
@@ -289,10 +310,12 @@ class DecoderModel:
                 mq, ms = ops.silu_mul_fp8(gu)
                 x = self.tp.all_reduce_(ops.linear_fp8(mq, ms, L["down"], L["down_s"]))
             else:
-                x = self.tp.all_reduce_(ops.linear(attn, L["o"]))
-                h, residual = ops.add_rmsnorm(x, residual, L["ln2"], c.rms_eps)
+                h, residual = self.tp.all_reduce_add_rmsnorm(ops.linear(attn, L["o"]), residual, L["ln2"],
+                                                             c.rms_eps, ops)
                 gu = ops.linear(h, L["gate_up"])
-                x = self.tp.all_reduce_(ops.linear(ops.silu_mul(gu), L["down"]))
+                x = ops.linear(ops.silu_mul(gu), L["down"])  # partial: reduced at the next norm
+        if not fp8:
+            x = self.tp.all_reduce_(x)
         if meta.logits_idx is not None:
             x = x.index_select(0, meta.logits_idx)
             residual = residual.index_select(0, meta.logits_idx)

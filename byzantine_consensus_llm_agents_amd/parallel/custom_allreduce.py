@@ -61,7 +61,9 @@ def _lib():
            "bcg_ar_take_error": [vp],
            "bcg_ar_error_async": [vp, vp, vp],
            "bcg_ar_set_error": [vp],
-           "bcg_ar_allreduce": [P, P, c_int, c_int, vp, vp, c_int64, c_int64, c_int, c_int, c_double, vp]}
+           "bcg_ar_allreduce": [P, P, c_int, c_int, vp, vp, c_int64, c_int64, c_int, c_int, c_double, vp],
+           "bcg_ar_allreduce_addnorm": [P, P, c_int, c_int, vp, vp, vp, vp, c_int, c_int, ctypes.c_float,
+                                        c_int64, c_int, c_double, vp]}
     for name, argtypes in sig.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
@@ -118,6 +120,31 @@ class _Rank:
         """Mark this rank's group broken (tests of the timeout path)."""
         if self.lib.bcg_ar_set_error(self._sig[self.rank]) != 0:
             raise RuntimeError("bcg_ar_set_error failed")
+
+    def can_addnorm(self, x: torch.Tensor) -> bool:
+        return (self.can(x) and x.dim() == 2 and x.shape[1] % 8 == 0 and x.shape[1] <= THREADS * 16)
+
+    def all_reduce_add_rmsnorm(self, x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                               stream=None) -> torch.Tensor:
+        """residual <- residual + sum_ranks(x); returns rmsnorm(residual) * w (one kernel, one-shot)."""
+        if not self.can_addnorm(x):
+            raise ValueError("fused all-reduce + RMSNorm: contiguous bf16 [rows, H<=8192], within the cap")
+        rows, H = x.shape
+        if not (residual.shape == x.shape and residual.is_contiguous() and residual.dtype == torch.bfloat16
+                and w.shape == (H,) and w.dtype == torch.bfloat16):
+            raise ValueError("fused all-reduce + RMSNorm: residual [rows, H] bf16, weight [H] bf16")
+        h = torch.empty_like(x)
+        blocks = int(min(self.max_blocks, rows))
+        s = (stream or torch.cuda.current_stream()).cuda_stream
+        rc = self.lib.bcg_ar_allreduce_addnorm(self._data, self._sig, self.rank, self.world,
+                                               ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(residual.data_ptr()),
+                                               ctypes.c_void_p(w.data_ptr()), ctypes.c_void_p(h.data_ptr()), rows,
+                                               H, float(eps), self.cap_bytes, blocks, self.timeout_s,
+                                               ctypes.c_void_p(s))
+        if rc != 0:
+            raise RuntimeError(f"bcg_ar_allreduce_addnorm launch failed (rc={rc})")
+        self.calls[3] = self.calls.get(3, 0) + 1
+        return h
 
     def take_error(self) -> bool:
         """True if a barrier of this rank timed out since the last check (synchronising)."""

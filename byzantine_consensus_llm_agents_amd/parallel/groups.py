@@ -118,7 +118,8 @@ def tensor_parallel_group(tp: int, custom_allreduce: bool = False) -> TPGroup:
     if custom_allreduce and mode != "0" and (mode == "force" or dist.get_backend(_TP_GROUPS[tp]) == "nccl"):
         if tp not in _CUSTOM_AR:
             from .custom_allreduce import XGMIAllReduce
-            _CUSTOM_AR[tp] = XGMIAllReduce(_TP_GROUPS[tp])
+            _CUSTOM_AR[tp] = XGMIAllReduce(_TP_GROUPS[tp],
+                                           timeout_s=float(os.environ.get("BCG_AR_TIMEOUT_S", "30")))
         custom = _CUSTOM_AR[tp]
     return TPGroup(_TP_GROUPS[tp], lay.tp_rank, tp, custom=custom, ctrl=_TP_CTRL[tp],
                    leader=lay.rank - lay.tp_rank)

@@ -11,7 +11,9 @@
 //               locally (ideal for <= ~1 MiB: one hop, n-1 links in parallel);
 //   two-shot  : reduce-scatter (rank r reduces slice r from every peer) +
 //               all-gather (read the other reduced slices from their owners):
-//               2(n-1)/n of the message per rank, spread over all n-1 links.
+//               2(n-1)/n of the message per rank, spread over all n-1 links;
+//   addnorm   : one-shot fused with the residual update + RMSNorm that follows
+//               the row-parallel o/down projections (one kernel, rows per block).
 //
 // Hand-off protocol (MI355X_MICROARCH.md "inter-workgroup visibility", at
 // system instead of agent scope because the consumer is another GPU):
@@ -186,6 +188,69 @@ __global__ __launch_bounds__(AR_THREADS) void ar_twoshot_kernel(ArPeers P, int r
   ar_end(me);
 }
 
+// One-shot all-reduce fused with the residual update and RMSNorm of the rows (TP decode:
+// the o_proj / down_proj partials of every rank -> residual += sum; h = rmsnorm(residual)).
+// A block owns whole rows (rows b, b + nblk, ...), so the row statistics never leave it.
+// Roundings follow the unfused pair exactly: sum -> bf16, residual + bf16(sum) -> bf16,
+// normalise the stored residual -- bitwise identical to all-reduce + add_rmsnorm.
+constexpr int AR_ROW_VECS = 2;  // H <= AR_THREADS * 8 * AR_ROW_VECS = 8192
+
+template <int W>
+__global__ __launch_bounds__(AR_THREADS) void ar_oneshot_addnorm_kernel(
+    ArPeers P, int rank, const u16x8* __restrict__ in, u16x8* residual, const u16x8* __restrict__ w,
+    u16x8* __restrict__ h_out, int rows, int hv /* H / 8 */, float eps, int64_t cap_vec, uint64_t timeout_ticks) {
+  __shared__ float s_part[AR_THREADS / WAVE];
+  ArSignal* me = P.sig[rank];
+  const uint32_t epoch = ar_begin(me);
+  const int64_t off = static_cast<int64_t>(epoch & 1u) * 2 * cap_vec;
+  u16x8* mine = P.data[rank] + off;
+  for (int r = blockIdx.x; r < rows; r += gridDim.x)
+    for (int i = threadIdx.x; i < hv; i += AR_THREADS) mine[static_cast<int64_t>(r) * hv + i] = in[static_cast<int64_t>(r) * hv + i];
+  ar_signal(P, rank, W, 0, epoch);
+  ar_wait(P, rank, W, 0, epoch, timeout_ticks);
+  for (int r = blockIdx.x; r < rows; r += gridDim.x) {
+    float v[AR_ROW_VECS][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < AR_ROW_VECS; ++c) {
+      const int i = threadIdx.x + c * AR_THREADS;
+      if (i < hv) {
+        const int64_t e = static_cast<int64_t>(r) * hv + i;
+        const u16x8 sum = ar_sum<W>(P, off, e);
+        const u16x8 res = residual[e];
+        u16x8 nr;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          nr[j] = f2bf(bf2f(res[j]) + bf2f(sum[j]));
+          v[c][j] = bf2f(nr[j]);
+          ss += v[c][j] * v[c][j];
+        }
+        residual[e] = nr;
+      }
+    }
+    ss = wave_sum(ss);
+    if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < AR_THREADS / WAVE; ++k) tot += s_part[k];
+    const float inv = rsqrtf(tot / (hv * 8) + eps);
+#pragma unroll
+    for (int c = 0; c < AR_ROW_VECS; ++c) {
+      const int i = threadIdx.x + c * AR_THREADS;
+      if (i < hv) {
+        const u16x8 wv = w[i];
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(v[c][j] * inv * bf2f(wv[j]));
+        h_out[static_cast<int64_t>(r) * hv + i] = o;
+      }
+    }
+    __syncthreads();  // s_part reused by the next row
+  }
+  ar_end(me);
+}
+
 template <int W>
 int launch_ar(const ArPeers& P, int rank, const void* in, void* out, int64_t nvec, int64_t cap_vec, int mode,
               int blocks, uint64_t ticks, hipStream_t stream) {
@@ -269,6 +334,46 @@ BCG_API int bcg_ar_set_error(void* sig) {
   ArSignal* s = static_cast<ArSignal*>(sig);
   const uint32_t one = 1;
   return hipMemcpy(&s->error, &one, sizeof(one), hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+
+// Fused one-shot all-reduce + residual add + RMSNorm over [rows, H] bf16 (see the kernel).
+BCG_API int bcg_ar_allreduce_addnorm(void* const* data, void* const* sig, int rank, int world, const void* in,
+                                     void* residual, const void* weight, void* h_out, int rows, int H, float eps,
+                                     int64_t cap_bytes, int blocks, double timeout_s, hipStream_t stream) {
+  if (world < 2 || world > AR_MAX_RANKS || (world & (world - 1)) || rank < 0 || rank >= world) return -2;
+  if (rows <= 0 || H % 8 || H > AR_THREADS * 8 * AR_ROW_VECS || static_cast<int64_t>(rows) * H * 2 > cap_bytes)
+    return -2;
+  if (blocks < 1 || blocks > AR_MAX_BLOCKS || cap_bytes % 16) return -2;
+  ArPeers P{};
+  for (int r = 0; r < world; ++r) {
+    if (!data[r] || !sig[r]) return -2;
+    P.data[r] = static_cast<u16x8*>(data[r]);
+    P.sig[r] = static_cast<ArSignal*>(sig[r]);
+  }
+  int dev = 0, khz = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+  const uint64_t ticks = static_cast<uint64_t>(timeout_s * 1e3 * khz);
+  const int64_t cap_vec = cap_bytes / 16;
+  const u16x8* src = static_cast<const u16x8*>(in);
+  u16x8* res = static_cast<u16x8*>(residual);
+  const u16x8* wv = static_cast<const u16x8*>(weight);
+  u16x8* ho = static_cast<u16x8*>(h_out);
+  const int hv = H / 8;
+  switch (world) {
+    case 2:
+      hipLaunchKernelGGL(ar_oneshot_addnorm_kernel<2>, dim3(blocks), dim3(AR_THREADS), 0, stream, P, rank, src, res,
+                         wv, ho, rows, hv, eps, cap_vec, ticks);
+      break;
+    case 4:
+      hipLaunchKernelGGL(ar_oneshot_addnorm_kernel<4>, dim3(blocks), dim3(AR_THREADS), 0, stream, P, rank, src, res,
+                         wv, ho, rows, hv, eps, cap_vec, ticks);
+      break;
+    default:
+      hipLaunchKernelGGL(ar_oneshot_addnorm_kernel<8>, dim3(blocks), dim3(AR_THREADS), 0, stream, P, rank, src, res,
+                         wv, ho, rows, hv, eps, cap_vec, ticks);
+  }
+  return BCG_CHECK_LAUNCH();
 }
 
 // n: bf16 elements (multiple of 8); mode 1 = one-shot, 2 = two-shot.

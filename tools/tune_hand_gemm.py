@@ -114,7 +114,8 @@ def main():
                 for sk in SPLITS:
                     if not hip.gemm_plan.supported(c, M, N, K, epi, sk):
                         continue
-                    if sk > 1 and (tiles * sk > 1024 or tiles >= 512 or K // 64 // sk < 6):
+                    # split-K: fill the rounds of 256 workgroups; never more than ~8 rounds
+                    if sk > 1 and (tiles * sk > 2304 or K // 64 // sk < 6):
                         continue
                     if epi == 2:
                         rr = torch.zeros(M, N, device="cuda", dtype=torch.bfloat16)
