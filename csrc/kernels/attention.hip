@@ -19,7 +19,7 @@
 //   are 16 contiguous bytes of one V^T row (block h>>1, offset 8(h&1)).
 //   K tiles load row r from token 8(r>>2) + 4u + (r&3) (a row gather: free).
 //
-// Decode: one workgroup per (sequence, kv head, split); the G = n_q/n_kv query
+// Decode: one workgroup per (sequence, kv head, 256-token split); the G = n_q/n_kv query
 // heads of the kv head share every K/V byte (GQA packing: 5 for Qwen3-14B);
 // waves are combined through LDS and splits merged by a second kernel
 // (flash-decoding).  Prefill: one workgroup per (64-query tile, query
@@ -229,23 +229,26 @@ struct Causal {
 };
 
 // ------------------------------------------------------------------ decode
-// Work item = (sequence b, 128-token split, kv head): the 4 waves of a
-// workgroup take the item's four 32-token chunks (one each, loaded with 16
-// back-to-back 16-B loads), and the G = n_q / n_kv query heads of the kv head
+// Work item = (sequence b, CPW*128-token split, kv head): the 4 waves of a
+// workgroup take CPW consecutive 32-token chunks each (all CPW x 16 16-B loads
+// issued before the first MFMA), and the G = n_q / n_kv query heads of the kv head
 // share every K/V byte (GQA packing).  Items are enumerated from the LIVE
-// context lengths -- a prefix sum over ceil(ctx_b / 128) computed by every
+// context lengths -- a prefix sum over ceil(ctx_b / split) computed by every
 // workgroup into LDS -- and a fixed grid strides over them.  A grid sized from
 // the block-table width instead (graph-safe, but ctx << max_model_len) spent
 // most of its workgroups reading seq_lens only to exit: 78 % of the launch at
 // B = 160, ctx 1700, max_model_len 8192.
-constexpr int DEC_SPLIT = DEC_WAVES * CHUNK;  // 128 tokens per item
 constexpr int DEC_MAX_B = 1024;
 
-template <int HD, bool KT = false, bool F8 = false>
+template <int HD, bool KT = false, bool F8 = false, int CPW = 1>
 __global__ __launch_bounds__(256) void decode_attn_kernel(
     const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
     const int* __restrict__ seq_lens, int B, int n_q, float scale_log2, float* __restrict__ part_o,
     float* __restrict__ part_ml, int max_splits) {
+  // CPW chunks per wave: an item covers DEC_WAVES * CPW * 32 tokens; every chunk's loads of
+  // a wave are issued before its first MFMA (CPW x 16 loads in flight per wave), and the
+  // split partials / merge traffic shrink by CPW
+  constexpr int DEC_SPLIT = DEC_WAVES * CHUNK * CPW;
   __shared__ int s_pre[DEC_MAX_B + 1];
   __shared__ int s_wsum[DEC_WAVES];
   __shared__ float s_ml[DEC_WAVES][2][16];
@@ -304,16 +307,23 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
 #pragma unroll
     for (int dt = 0; dt < HD / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int t0 = start + w * CHUNK;
-    if (t0 < ctx) {  // wave-uniform
-      const int last_blk = (ctx - 1) / BS;
-      const int e0 = table[t0 / BS], e1 = table[min(t0 / BS + 1, last_blk)];
-      Chunk<HD, F8> c;
-      load_chunk<HD, KT, F8>(c, g, e0, e1, kvh, lane);
-      if (t0 + CHUNK <= ctx)  // wave-uniform: a full chunk needs no tail masking
-        compute_chunk<HD, AllVisible, false, F8>(c, bq, t0, ctx, AllVisible{}, scale_log2, m, l, o, lane);
+    const int t0 = start + w * CHUNK * CPW;
+    const int last_blk = (ctx - 1) / BS;
+    Chunk<HD, F8> c[CPW];
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) {
+      const int tj = t0 + j * CHUNK;
+      if (tj < ctx)  // wave-uniform
+        load_chunk<HD, KT, F8>(c[j], g, table[tj / BS], table[min(tj / BS + 1, last_blk)], kvh, lane);
+    }
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) {
+      const int tj = t0 + j * CHUNK;
+      if (tj >= ctx) break;  // wave-uniform
+      if (tj + CHUNK <= ctx)  // wave-uniform: a full chunk needs no tail masking
+        compute_chunk<HD, AllVisible, false, F8>(c[j], bq, tj, ctx, AllVisible{}, scale_log2, m, l, o, lane);
       else
-        compute_chunk<HD, AllVisible, true, F8>(c, bq, t0, ctx, AllVisible{}, scale_log2, m, l, o, lane);
+        compute_chunk<HD, AllVisible, true, F8>(c[j], bq, tj, ctx, AllVisible{}, scale_log2, m, l, o, lane);
     }
 
     // combine the 4 waves through LDS
@@ -372,9 +382,10 @@ __global__ __launch_bounds__(HD) void decode_combine_kernel(const float* __restr
   out[static_cast<size_t>(bq) * HD + d] = f2bf(ll > 0.f ? oo / ll : 0.f);
 }
 
-template <int HD, bool KT = false, bool F8 = false>
+template <int HD, bool KT = false, bool F8 = false, int CPW = 1>
 void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks, const int* seq_lens, int B,
                    int n_q, float sl, float* ws, int max_splits, bf16_t* out, hipStream_t stream) {
+  constexpr int DEC_SPLIT = DEC_WAVES * CHUNK * CPW;
   float* part_o = ws;
   float* part_ml = ws + static_cast<size_t>(B) * n_q * max_splits * HD;
   // fixed (graph-safe) grid striding over the live items: one full wave of resident workgroups
@@ -383,11 +394,11 @@ void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
     int per_cu = 0, cus = 0, dev = 0;
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_attn_kernel<HD, KT, F8>, 256, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_attn_kernel<HD, KT, F8, CPW>, 256, 0);
     resident = std::max(1, per_cu) * std::max(1, cus);
   }
   const int grid = static_cast<int>(std::min<long>(static_cast<long>(B) * g.n_kv * max_splits, resident));
-  hipLaunchKernelGGL((decode_attn_kernel<HD, KT, F8>), dim3(grid), dim3(256), 0, stream, q, g, tables, max_blocks,
+  hipLaunchKernelGGL((decode_attn_kernel<HD, KT, F8, CPW>), dim3(grid), dim3(256), 0, stream, q, g, tables, max_blocks,
                      seq_lens, B, n_q, sl, part_o, part_ml, max_splits);
   hipLaunchKernelGGL(decode_combine_kernel<HD>, dim3(B * n_q), dim3(HD), 0, stream, part_o, part_ml, seq_lens,
                      n_q, max_splits, DEC_SPLIT, out);
@@ -691,12 +702,13 @@ int launch_prefill(int nt, int n_tiles, int n_q, const bf16_t* q, KVGeom g, cons
 
 }  // namespace
 
-// Split size for a decode batch.  Measured on MI355X (tools/bench_ops.py,
-// Qwen3-14B geometry, ctx 1700, B 40-192): one 32-token chunk per wave (128
-// tokens per work item) beats looping waves over several chunks (256-2048-token
-// splits: 2.0-2.6 TB/s against 3.0-3.2) -- more independent loads in flight
-// per CU at 3 waves/SIMD.
-BCG_API int bcg_decode_split_tokens(int B, int n_kv, int max_tokens) { return DEC_SPLIT; }
+// Split size for a decode batch.  Measured on MI355X (tools/bench_ops.py, Qwen3-14B
+// geometry, ctx 1700): two 32-token chunks per wave with BOTH chunks' loads issued
+// before the first MFMA (256-token items) stream 5.2-5.4 TB/s at B = 160-608, against
+// 4.4-4.7 for one chunk per wave (128-token items) -- and halve the split partials the
+// merge kernel reads.  (Looping a wave over chunks one at a time was slower: 2-2.6 TB/s.)
+constexpr int DEC_CPW = 2;
+BCG_API int bcg_decode_split_tokens(int B, int n_kv, int max_tokens) { return DEC_WAVES * CHUNK * DEC_CPW; }
 
 // kv_fp8: the caches hold OCP e4m3fn bytes (scale 1) instead of bf16.
 BCG_API int bcg_paged_attention_decode(const void* q, const void* k_cache, const void* v_cache, int layer,
@@ -705,21 +717,23 @@ BCG_API int bcg_paged_attention_decode(const void* q, const void* k_cache, const
                                        float scale, float* workspace, int max_splits, int split_tokens,
                                        void* out, int kv_fp8, hipStream_t stream) {
   if (block_size != BS || n_q % n_kv || n_q / n_kv > 16 || B <= 0 || B > DEC_MAX_B) return -2;
-  if (split_tokens != DEC_SPLIT || max_splits * split_tokens < max_blocks * BS) return -3;
+  if (split_tokens != DEC_WAVES * CHUNK * DEC_CPW || max_splits * split_tokens < max_blocks * BS) return -3;
   KVGeom g{static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), layer, num_blocks, n_kv};
   const bf16_t* qb = static_cast<const bf16_t*>(q);
   bf16_t* ob = static_cast<bf16_t*>(out);
   const float sl = scale * LOG2E;
   if (hd == 128 && kv_fp8) {
-    launch_decode<128, false, true>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace, max_splits,
-                                    ob, stream);
+    launch_decode<128, false, true, DEC_CPW>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace,
+                                             max_splits, ob, stream);
   } else if (hd == 128) {
-    launch_decode<128>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace, max_splits, ob, stream);
+    launch_decode<128, false, false, DEC_CPW>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace,
+                                              max_splits, ob, stream);
   } else if (hd == 64 && kv_fp8) {
-    launch_decode<64, false, true>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace, max_splits,
-                                   ob, stream);
+    launch_decode<64, false, true, DEC_CPW>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace,
+                                            max_splits, ob, stream);
   } else if (hd == 64) {
-    launch_decode<64>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace, max_splits, ob, stream);
+    launch_decode<64, false, false, DEC_CPW>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace,
+                                             max_splits, ob, stream);
   } else {
     return -2;
   }
@@ -733,10 +747,13 @@ BCG_API int bcg_paged_attention_decode_exp(const void* q, const void* k_cache, c
                                            const int* seq_lens, int B, int n_q, int hd, float scale,
                                            float* workspace, int max_splits, int split_tokens, void* out,
                                            int variant, hipStream_t stream) {
-  if (hd != 128 || n_q / n_kv > 16 || split_tokens != DEC_SPLIT || B > DEC_MAX_B) return -2;
+  if (hd != 128 || n_q / n_kv > 16 || split_tokens != DEC_WAVES * CHUNK || B > DEC_MAX_B) return -2;
   KVGeom g{static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), layer, num_blocks, n_kv};
   const float sl = scale * LOG2E;
-  if (variant == 1)
+  if (variant == 2)  // two chunks per wave, both loaded up front (256-token items)
+    launch_decode<128, false, false, 2>(static_cast<const bf16_t*>(q), g, block_tables, max_blocks, seq_lens, B,
+                                        n_q, sl, workspace, max_splits, static_cast<bf16_t*>(out), stream);
+  else if (variant == 1)
     launch_decode<128, true>(static_cast<const bf16_t*>(q), g, block_tables, max_blocks, seq_lens, B, n_q, sl,
                              workspace, max_splits, static_cast<bf16_t*>(out), stream);
   else

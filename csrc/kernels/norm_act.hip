@@ -71,23 +71,24 @@ __global__ __launch_bounds__(NORM_THREADS) void add_rmsnorm_kernel(
   }
 }
 
+// One 16-B vector of gate + up per thread and grid row-major over [T, I/8]: 32-bit
+// index math (a 64-bit div/mod per element was the kernel's main cost), fast exp.
 __global__ __launch_bounds__(256) void silu_mul_kernel(const bf16_t* __restrict__ gu,
-                                                       bf16_t* __restrict__ out, int64_t T, int I) {
-  const int64_t nvec_row = I / 8;
-  const int64_t total = T * nvec_row;
-  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
-       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int64_t r = i / nvec_row, c = i % nvec_row;
-    const bf16_t* g = gu + r * 2 * I + c * 8;
-    u16x8 gv = *reinterpret_cast<const u16x8*>(g);
-    u16x8 uv = *reinterpret_cast<const u16x8*>(g + I);
+                                                       bf16_t* __restrict__ out, int T, int I) {
+  const int nvec_row = I >> 3;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;  // vector within the row
+  if (c >= nvec_row) return;
+  for (int r = blockIdx.y; r < T; r += gridDim.y) {
+    const bf16_t* g = gu + static_cast<size_t>(r) * 2 * I + c * 8;
+    const u16x8 gv = *reinterpret_cast<const u16x8*>(g);
+    const u16x8 uv = *reinterpret_cast<const u16x8*>(g + I);
     u16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float a = bf2f(gv[j]);
-      o[j] = f2bf(a / (1.f + __expf(-a)) * bf2f(uv[j]));
+      o[j] = f2bf(__fdividef(a, 1.f + __expf(-a)) * bf2f(uv[j]));
     }
-    *reinterpret_cast<u16x8*>(out + r * I + c * 8) = o;
+    *reinterpret_cast<u16x8*>(out + static_cast<size_t>(r) * I + c * 8) = o;
   }
 }
 
@@ -116,9 +117,10 @@ BCG_API int bcg_embed_rmsnorm(const int* tokens, const void* table, const void* 
 
 BCG_API int bcg_silu_mul(const void* gu, void* out, int64_t T, int I, hipStream_t stream) {
   if (I % 8 != 0 || T <= 0) return -2;
-  const int64_t work = T * (I / 8);
-  const int blocks = static_cast<int>(std::min<int64_t>((work + 255) / 256, 256 * 16));
-  hipLaunchKernelGGL(silu_mul_kernel, dim3(blocks), dim3(256), 0, stream,
-                     static_cast<const bf16_t*>(gu), static_cast<bf16_t*>(out), T, I);
+  if (T > (1 << 30) || I > (1 << 27)) return -2;
+  const int bx = (I / 8 + 255) / 256;
+  const int by = static_cast<int>(std::min<int64_t>(T, std::max<int64_t>(1, 8192 / bx)));
+  hipLaunchKernelGGL(silu_mul_kernel, dim3(bx, by), dim3(256), 0, stream,
+                     static_cast<const bf16_t*>(gu), static_cast<bf16_t*>(out), static_cast<int>(T), I);
   return BCG_CHECK_LAUNCH();
 }
