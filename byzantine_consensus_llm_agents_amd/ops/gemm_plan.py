@@ -21,7 +21,8 @@ from typing import Dict, Optional, Tuple
 TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "engine", "tuned",
                      "hand_gemm.json")
 TILES = ((128, 128), (64, 128), (128, 64), (256, 128), (64, 256), (64, 64), (32, 128),  # csrc/kernels/gemm.hip CFGS
-         (256, 128), (128, 256), (128, 128))
+         (256, 128), (128, 256), (128, 128), (256, 256))
+PP_CFG = 10  # csrc/kernels/gemm_pp.hip: 256 x 256 ping-pong tile, N only a multiple of 16
 N_CFGS = len(TILES)
 SPLITS = (1, 2, 3, 4, 6, 8)
 
@@ -48,6 +49,8 @@ class GemmPlan:
         if cfg not in self.tiles or M <= 0 or K % 64 or K <= 0 or split_k < 1 or K // 64 < split_k:
             return False
         bn = self.tiles[cfg][1]
+        if cfg == PP_CFG:
+            return N % 16 == 0 and (epi != 1 or (N % 2 == 0 and (N // 2) % 128 == 0))
         if N % bn:
             return False
         if epi == 1 and (N % 2 or (N // 2) % (bn // 2)):

@@ -279,7 +279,7 @@ def hip_ops() -> SimpleNamespace:
         ws = cnt = None
         if split_k > 1:
             bm, bn = plan.tiles[cfg]
-            tiles = (M + bm - 1) // bm * (N // bn)
+            tiles = (M + bm - 1) // bm * ((N + bn - 1) // bn)
             _req(tiles <= (1 << 16), "gemm_nt: too many output tiles for split-K")
             ws = torch.empty(tiles * split_k * bm * bn, dtype=torch.float32, device=x.device)
             cnt = _counters(x.device)

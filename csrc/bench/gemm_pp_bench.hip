@@ -1,0 +1,91 @@
+// Standalone timing harness for csrc/kernels/gemm_pp.hip (one variant per binary: build-time
+// -D switches, so variants do not perturb each other's codegen -- cdna_hip_programming.md
+// §5.4 rule 19).  Random bf16 operands (hash-based, |x| < 1), weights rotated over copies
+// that exceed the 256 MiB Infinity Cache, hipEvent timing of back-to-back launches.
+//
+//   gemm_pp_bench M N K EPI SPLIT [ITERS]   -> one JSON line
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <vector>
+
+extern "C" int bcg_gemm_pp(int epi, const void* x, const void* w, const void* bias, const void* residual, void* c,
+                           void* ws, void* counters, int M, int N, int K, int inter, int split_k, hipStream_t stream);
+
+__global__ void fill_bf16(uint16_t* p, size_t n, uint32_t seed, float scale) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    const float v = ((h & 0xffffff) / 16777216.0f * 2.f - 1.f) * scale;
+    p[i] = (uint16_t)(__float_as_uint(v) >> 16);
+  }
+}
+
+#define CK(x)                                                         \
+  do {                                                                \
+    hipError_t e_ = (x);                                              \
+    if (e_ != hipSuccess) {                                           \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                        \
+    }                                                                 \
+  } while (0)
+
+int main(int argc, char** argv) {
+  if (argc < 6) {
+    fprintf(stderr, "usage: %s M N K EPI SPLIT [ITERS]\n", argv[0]);
+    return 2;
+  }
+  const int M = atoi(argv[1]), N = atoi(argv[2]), K = atoi(argv[3]), epi = atoi(argv[4]), split = atoi(argv[5]);
+  const int iters = argc > 6 ? atoi(argv[6]) : 20;
+  const size_t wbytes = (size_t)N * K * 2;
+  const int copies = (int)std::max<size_t>(2, std::min<size_t>(8, ((size_t)1 << 30) / wbytes + 1));
+  uint16_t *x, *r, *c;
+  std::vector<uint16_t*> w(copies);
+  CK(hipMalloc(&x, (size_t)M * K * 2));
+  CK(hipMalloc(&r, (size_t)M * N * 2));
+  CK(hipMalloc(&c, (size_t)M * N * 2));
+  hipLaunchKernelGGL(fill_bf16, dim3(1024), dim3(256), 0, 0, x, (size_t)M * K, 1u, 1.f);
+  hipLaunchKernelGGL(fill_bf16, dim3(1024), dim3(256), 0, 0, r, (size_t)M * N, 2u, 1.f);
+  for (int i = 0; i < copies; ++i) {
+    CK(hipMalloc(&w[i], wbytes));
+    hipLaunchKernelGGL(fill_bf16, dim3(1024), dim3(256), 0, 0, w[i], (size_t)N * K, 3u + i, 0.05f);
+  }
+  const int tiles = (M + 255) / 256 * ((N + 255) / 256);
+  float* ws = nullptr;
+  int* cnt = nullptr;
+  if (split > 1) {
+    CK(hipMalloc(&ws, (size_t)tiles * split * 65536 * 4));
+    CK(hipMalloc(&cnt, (size_t)tiles * 4));
+    CK(hipMemset(cnt, 0, (size_t)tiles * 4));
+  }
+  auto run = [&](int i) {
+    const void* res = epi == 2 ? r : nullptr;
+    void* out = epi == 2 ? (void*)r : (void*)c;
+    return bcg_gemm_pp(epi, x, w[i % copies], nullptr, res, out, ws, cnt, M, N, K, N / 2, split, 0);
+  };
+  for (int i = 0; i < 5; ++i)
+    if (run(i)) {
+      fprintf(stderr, "launch failed\n");
+      return 1;
+    }
+  CK(hipDeviceSynchronize());
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  CK(hipEventRecord(a, 0));
+  for (int i = 0; i < iters; ++i) run(i);
+  CK(hipEventRecord(b, 0));
+  CK(hipEventSynchronize(b));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, a, b));
+  const double us = ms * 1e3 / iters;
+  printf("{\"variant\": \"%s\", \"M\": %d, \"N\": %d, \"K\": %d, \"epi\": %d, \"split\": %d, \"us\": %.1f, "
+         "\"tflops\": %.1f}\n",
+         VARIANT_NAME, M, N, K, epi, split, us, 2.0 * M * N * K / us / 1e6);
+  return 0;
+}

@@ -328,15 +328,23 @@ int dispatch(int cfg, const void* x, const void* w, const void* bias, const void
 
 }  // namespace
 
-// Tile configurations: see CFGS (BM x BN, pipeline stages).
+BCG_API int bcg_gemm_pp(int epi, const void* x, const void* w, const void* bias, const void* residual, void* c,
+                        void* ws, void* counters, int M, int N, int K, int inter, int split_k, hipStream_t stream);
+constexpr int PP_CFG = N_CFG;  // the 256 x 256 ping-pong kernel (gemm_pp.hip)
+
+// Tile configurations: see CFGS (BM x BN, pipeline stages); PP_CFG = gemm_pp.hip.
 BCG_API int bcg_gemm_tile(int cfg, int* bm, int* bn) {
+  if (cfg == PP_CFG) {
+    *bm = *bn = 256;
+    return 0;
+  }
   if (cfg < 0 || cfg >= N_CFG) return -2;
   *bm = CFGS[cfg].bm;
   *bn = CFGS[cfg].bn;
   return 0;
 }
 
-BCG_API int bcg_gemm_num_cfgs() { return N_CFG; }
+BCG_API int bcg_gemm_num_cfgs() { return N_CFG + 1; }
 
 // epi: 0 = store (+bias), 1 = silu(gate)*up into [M, inter], 2 = residual + acc.
 // split_k > 1: fp32 partial tiles in `ws` (>= m_tiles*n_tiles*split_k*BM*BN floats) and one
@@ -346,6 +354,7 @@ BCG_API int bcg_gemm_num_cfgs() { return N_CFG; }
 BCG_API int bcg_gemm_nt(int cfg, int epi, const void* x, const void* w, const void* bias, const void* residual,
                         void* c, void* ws, void* counters, int M, int N, int K, int inter, int split_k,
                         hipStream_t stream) {
+  if (cfg == PP_CFG) return bcg_gemm_pp(epi, x, w, bias, residual, c, ws, counters, M, N, K, inter, split_k, stream);
   if (M <= 0 || K % BK || K <= 0 || split_k < 1 || K / BK < split_k) return -2;
   if (split_k > 1 && (!ws || !counters)) return -2;
   int bm, bn;

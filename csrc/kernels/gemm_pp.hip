@@ -1,0 +1,363 @@
+// 256 x 256 x 64 "ping-pong" GEMM on CDNA4 matrix cores (gfx950), fused epilogues.
+//
+//   C[M, N] = X[M, K] · W[N, K]^T            (bf16 in, fp32 accumulate, bf16 out)
+//
+// The big-tile sibling of gemm.hip for the projections that are large enough to fill the
+// chip with 256 x 256 tiles: prefill chunks (M = 16384) and the wide decode buckets
+// (M = 448..768: gate_up, LM head; qkv / o / down with split-K).  SURVEY.md §2.3
+// K-GEMM-QKV/O/GU/D/LMH; the reference reaches these GEMMs inside vLLM
+// (byzantine_consensus_game/vllm_agent.py:430).
+//
+// Structure (cdna_hip_programming.md "The 256² 8-phase template", rebuilt here):
+//   * one workgroup = 8 waves = 2 groups of 4 (group g owns output rows g*128..+128, wave
+//     wc of the group owns columns wc*64..+64): per wave 128 x 64 = 8 x 4 blocks of 16x16,
+//     128 accumulator VGPRs;
+//   * a K-tile (64 deep) is staged as four 16-KiB "half" slots, each filled by ONE
+//     glds pair per thread (`global_load_lds`, 16 B per lane, no VGPR round trip):
+//       A-lo = X rows {0..63, 128..191}, A-hi = X rows {64..127, 192..255},
+//       B-lo = W rows {wc*64 + 0..31},   B-hi = W rows {wc*64 + 32..63};
+//     the LDS holds two K-tiles (128 KiB, one workgroup per CU);
+//   * a K-tile is computed in 4 phases of 16 MFMAs (one 64 x 32 quadrant of the wave's
+//     tile x 64 of K):  j0: read A-lo + B-lo, MFMA(lo, lo) · j1: read B-hi, MFMA(lo, hi) ·
+//     j2: read A-hi, MFMA(hi, hi) · j3: (no reads) MFMA(hi, lo);
+//   * ping-pong: group 1 runs one barrier behind group 0, so on every SIMD (one wave of
+//     each group) one wave issues its MFMAs while the other issues its LDS reads and its
+//     glds -- each phase is   reads -> glds -> counted vmcnt -> s_barrier -> lgkmcnt(0)
+//     -> 16 MFMA -> s_barrier;
+//   * every phase issues exactly one half-slot load, 6 phases ahead of its first read:
+//       j0: B-hi(t+1)   j1: A-hi(t+1)   j2: A-lo(t+2)   j3: B-lo(t+2)
+//     and the reads are j0: B-lo(t), j1: B-hi(t), j2: A-hi(t), j3: A-lo(t+1) (4, 4, 8, 8)
+//     With loads issued in phase p and the wait before phase r's first barrier covering
+//     the loads of phases <= r-4 (vmcnt(8): 4 half-slots in flight per wave), a load is
+//     visible to the readers of phase >= p+5 and a slot is refilled >= 2 phases after its
+//     last read -- the two orderings the schedule above satisfies with zero slack at
+//     B-hi/B-lo (derivation in PERF.md, "ping-pong GEMM");
+//   * LDS rows are 128 B with the 16-B chunk c of row r at chunk c ^ ((r >> 1) & 7) (the
+//     swizzle of gemm.hip: conflict-free fragment ds_read_b128); glds writes linearly, so
+//     the swizzle is applied to each lane's SOURCE address;
+//   * the operands are swapped in the MFMA (W fragment as A, X as B) so a lane holds 4
+//     consecutive output columns of one row: 8-B stores, gate/up pairs in one lane;
+//   * XCD-aware tile order (bijective remap): the m-tiles and K-splits of one n-tile run
+//     on one XCD, so each weight byte comes from HBM once;
+//   * split-K: fp32 partial tiles stored write-through (sc1), last arriver reduces
+//     (as gemm.hip, cdna_hip_programming.md §6 Guideline 16 R1).
+#include "common.h"
+
+#ifndef PP_GROUP_M
+#define PP_GROUP_M 8  // m-tiles per tile-order group (L2 reuse of both operands at prefill M)
+#endif
+
+namespace {
+
+constexpr int PBM = 256, PBN = 256, PBK = 64;
+constexpr int HALF = 128 * 128;  // one half slot: 128 rows x 128 B
+constexpr int BUF = 4 * HALF;    // one K-tile: A-lo, B-lo, B-hi, A-hi
+enum { S_ALO = 0, S_BLO = 1, S_BHI = 2, S_AHI = 3 };
+enum Epilogue { EPI_STORE = 0, EPI_SILU_MUL = 1, EPI_RESIDUAL = 2 };
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+__device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
+
+__device__ __forceinline__ void sbar() {
+#ifndef PP_NO_SCHED_BARRIER
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+#ifndef PP_ABL_NOBAR
+  __builtin_amdgcn_s_barrier();
+#endif
+#ifndef PP_NO_SCHED_BARRIER
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ W, const bf16_t* __restrict__ bias,
+    const bf16_t* __restrict__ residual, bf16_t* __restrict__ C, float* __restrict__ ws,
+    int* __restrict__ counters, int M, int N, int K, int ldc, int inter, int m_tiles, int n_tiles,
+    int split_k) {
+  // ONE shared array (a second __shared__ object can make hipcc drain vmcnt before every
+  // ds_read: cdna_hip_programming.md "Projection GEMM" item 4a)
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
+
+  // ---- XCD-aware order: bijective remap, then (n-tile, m-tile, k-split) ----
+  const int nwg = m_tiles * n_tiles * split_k;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, rem = nwg & 7;
+  const int r_id = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (bid >> 3);
+  const int split = r_id % split_k;
+  const int tile = r_id / split_k;
+  // grouped order: PP_GROUP_M m-tiles x all n-tiles per group, m fastest -- an XCD's ~32
+  // resident tiles then cover ~8 m x 4 n (X and W both L2-reused); decode (m_tiles <= 8)
+  // degenerates to "the m-tiles of one n-tile together"
+  const int grp = tile / (PP_GROUP_M * n_tiles), in_grp = tile % (PP_GROUP_M * n_tiles);
+  const int gm = min(m_tiles - grp * PP_GROUP_M, PP_GROUP_M);
+  const int m_tile = grp * PP_GROUP_M + in_grp % gm, n_tile = in_grp / gm;
+  const int m0 = m_tile * PBM, n0 = n_tile * PBN;
+  const int nk_all = K / PBK;
+  const int kt0 = split * nk_all / split_k;
+  const int nk = (split + 1) * nk_all / split_k - kt0;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // global row of slot row s (0..127) of each half slot
+  auto w_row = [&](int r) {  // r: tile row of W (0..255)
+    if constexpr (EPI == EPI_SILU_MUL) {  // 16-row blocks alternate gate / up of the same features
+      const int blk = r >> 4;
+      const int feat = (n0 >> 1) + (blk >> 1) * 16 + (r & 15);
+      return (blk & 1) ? inter + feat : feat;
+    } else {
+      return min(n0 + r, N - 1);  // clamped rows are never stored
+    }
+  };
+  // each thread stages 2 x 16 B of a half slot: rows (wave*2 + i)*8 + lane/8, chunk slot lane%8
+  const int st_r0 = wave * 16 + (lane >> 3);
+  const int st_phys = lane & 7;
+  uint32_t offA[2][2], offB[2][2];  // [hi][i]: element offsets of the rows (k offset added per tile)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int s = st_r0 + i * 8;
+    const int c = st_phys ^ ((s >> 1) & 7);
+#pragma unroll
+    for (int hi = 0; hi < 2; ++hi) {
+      const int am = min(m0 + (s >> 6) * 128 + hi * 64 + (s & 63), M - 1);
+      offA[hi][i] = static_cast<uint32_t>(am) * K + c * 8;
+      const int bn = w_row((s >> 5) * 64 + hi * 32 + (s & 31));
+      offB[hi][i] = static_cast<uint32_t>(bn) * K + c * 8;
+    }
+  }
+  auto load_half = [&](int t, int slot) {  // K-tile t (relative) -> buffer t & 1, half `slot`
+#ifdef PP_ABL_NOLOAD
+    if (t >= 2) return;
+#endif
+    unsigned char* dst = smem + (t & 1) * BUF + slot * HALF + wave * 2048;
+    const uint32_t k0 = (kt0 + t) * PBK;
+    const bf16_t* base = (slot == S_ALO || slot == S_AHI) ? X : W;
+    const uint32_t* off = slot == S_ALO ? offA[0] : slot == S_AHI ? offA[1] : slot == S_BLO ? offB[0] : offB[1];
+    __builtin_amdgcn_global_load_lds(base + (off[0] + k0), dst, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(base + (off[1] + k0), dst + 1024, 16, 0, 0);
+  };
+
+  f32x4 acc[4][8];  // [n-block][m-block]
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // [block][k-step]; alo/ahi: A-lo / A-hi fragments (A-lo of tile t+1 is read in phase j3 of
+  // tile t, beside that phase's MFMAs on A-hi: per-phase reads 4, 4, 8, 8 instead of 12, 4, 8, 0)
+  bf16x8 alo[4][2], ahi[4][2], blo[2][2], bhi[2][2];
+  auto read_a = [&](int t, int slot, bf16x8 (&a)[4][2]) {
+#ifdef PP_ABL_NOREAD
+    if (t >= 1) return;
+#endif
+    const unsigned char* base = smem + (t & 1) * BUF + slot * HALF;
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int r = g * 64 + mb * 16 + fr;
+        a[mb][s] = *reinterpret_cast<const bf16x8*>(base + r * 128 + swz(r, 4 * s + fq) * 16);
+      }
+  };
+  auto read_b = [&](int t, int slot, bf16x8 (&b)[2][2]) {
+#ifdef PP_ABL_NOREAD
+    if (t >= 1) return;
+#endif
+    const unsigned char* base = smem + (t & 1) * BUF + slot * HALF;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int r = wc * 32 + nb * 16 + fr;
+        b[nb][s] = *reinterpret_cast<const bf16x8*>(base + r * 128 + swz(r, 4 * s + fq) * 16);
+      }
+  };
+  auto mfma = [&](int nh, int mh, const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2]) {
+#ifndef PP_NO_SETPRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+          acc[nh * 2 + nb][mh * 4 + mb] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nb][s], a[mb][s], acc[nh * 2 + nb][mh * 4 + mb], 0, 0, 0);
+#ifndef PP_NO_SETPRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+  };
+  // counted wait before the phase's first barrier: loads of phases <= p-4 landed
+  auto vm_wait = [&](bool full_window) {
+    if (full_window) {
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  };
+  auto mma_block = [&](int nh, int mh, const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2]) {
+    sbar();  // pre-barrier
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mfma(nh, mh, a, b);
+    sbar();  // post-barrier
+  };
+
+  // ---- prologue: phases -6..-1 ----
+  load_half(0, S_ALO);
+  load_half(0, S_BLO);
+  load_half(0, S_BHI);
+  load_half(0, S_AHI);
+  if (nk > 1) {
+    load_half(1, S_ALO);
+    load_half(1, S_BLO);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A-lo(0), B-lo(0) landed
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  sbar();
+  if (g == 1) sbar();  // group 1 runs one barrier behind group 0
+  read_a(0, S_ALO, alo);  // phase j3 of "tile -1"
+
+  for (int t = 0; t < nk; ++t) {
+    const bool l1 = t + 1 < nk, l2 = t + 2 < nk;
+    // j0: B-lo; load B-hi(t+1)
+    read_b(t, S_BLO, blo);
+    if (l1) load_half(t + 1, S_BHI);
+    vm_wait(l1);
+    mma_block(0, 0, alo, blo);
+    // j1: B-hi; load A-hi(t+1)
+    read_b(t, S_BHI, bhi);
+    if (l1) load_half(t + 1, S_AHI);
+    vm_wait(l1);
+    mma_block(1, 0, alo, bhi);
+    // j2: A-hi; load A-lo(t+2)
+    read_a(t, S_AHI, ahi);
+    if (l2) load_half(t + 2, S_ALO);
+    vm_wait(l2);
+    mma_block(1, 1, ahi, bhi);
+    // j3: A-lo(t+1) (loaded in phase 4t-2: visible from phase 4t+3); load B-lo(t+2)
+    if (l1) read_a(t + 1, S_ALO, alo);
+    if (l2) load_half(t + 2, S_BLO);
+    vm_wait(l2);
+    mma_block(0, 1, ahi, blo);
+  }
+  if (g == 0) sbar();  // balance group 1's extra barrier
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // ---- split-K: partial tiles -> workspace (write-through); the last arriver reduces ----
+  if (split_k > 1) {
+    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+    float* slab = ws + static_cast<size_t>(tile) * split_k * (PBM * PBN);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(slab, 0, split_k * PBM * PBN * 4, 0x00020000);
+    __syncthreads();  // every wave is past its last ds_read: smem is reusable as the flag slot
+    int* flag = reinterpret_cast<int*>(smem);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int off = (split * (PBM * PBN) + ((wave * 4 + i) * 8 + j) * 256 + lane * 4) * 4;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, acc[i][j]), rs, off, 0, 16 /*sc1*/);
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int prev = __hip_atomic_fetch_add(&counters[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == split_k - 1;
+      if (last) __hip_atomic_store(&counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int sp = 0; sp < split_k; ++sp) {
+      if (sp == split) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int off = (sp * (PBM * PBN) + ((wave * 4 + i) * 8 + j) * 256 + lane * 4) * 4;
+          acc[i][j] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16 /*sc1*/));
+        }
+    }
+  }
+
+  // ---- epilogue: lane holds D[n = 4fq + e][m = fr] of block (nb, mb) ----
+#pragma unroll
+  for (int mb = 0; mb < 8; ++mb) {
+    const int m = m0 + g * 128 + mb * 16 + fr;
+    if (m >= M) continue;
+    if constexpr (EPI == EPI_SILU_MUL) {
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh) {  // (gate, up) block pairs of the same 16 features
+        const int feat = (n0 >> 1) + (wc * 2 + nh) * 16 + 4 * fq;
+        u16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = f2bf(silu(acc[2 * nh][mb][e]) * acc[2 * nh + 1][mb][e]);
+        *reinterpret_cast<u16x4*>(C + static_cast<size_t>(m) * ldc + feat) = o;
+      }
+    } else {
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const int n = n0 + wc * 64 + nb * 16 + 4 * fq;
+        if (n >= N) continue;
+        float v[4] = {acc[nb][mb][0], acc[nb][mb][1], acc[nb][mb][2], acc[nb][mb][3]};
+        if (bias != nullptr) {
+          const u16x4 b = *reinterpret_cast<const u16x4*>(bias + n);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += bf2f(b[e]);
+        }
+        if constexpr (EPI == EPI_RESIDUAL) {
+          const u16x4 rr = *reinterpret_cast<const u16x4*>(residual + static_cast<size_t>(m) * ldc + n);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += bf2f(rr[e]);
+        }
+        u16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+        *reinterpret_cast<u16x4*>(C + static_cast<size_t>(m) * ldc + n) = o;
+      }
+    }
+  }
+}
+
+template <int EPI>
+int launch_pp(const void* x, const void* w, const void* bias, const void* res, void* c, float* ws, int* cnt, int M,
+              int N, int K, int inter, int split_k, hipStream_t stream) {
+  const int m_tiles = (M + PBM - 1) / PBM, n_tiles = (N + PBN - 1) / PBN;
+  const int ldc = EPI == EPI_SILU_MUL ? inter : N;
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI>), dim3(m_tiles * n_tiles * split_k), dim3(512), 0, stream,
+                     static_cast<const bf16_t*>(x), static_cast<const bf16_t*>(w), static_cast<const bf16_t*>(bias),
+                     static_cast<const bf16_t*>(res), static_cast<bf16_t*>(c), ws, cnt, M, N, K, ldc, inter, m_tiles,
+                     n_tiles, split_k);
+  return BCG_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+// epi: 0 = store (+bias), 1 = silu(gate)*up into [M, inter], 2 = residual + acc.
+// Requirements: K % 64 == 0, K/64 >= split_k; N % 16 == 0 (a partial last n-tile is masked);
+// EPI 1: N == 2*inter, inter % 128 == 0.  split_k > 1: `ws` >= m_tiles*n_tiles*split_k*65536
+// floats, `counters` >= m_tiles*n_tiles zeroed ints (left zeroed).  Pointers 16-B aligned.
+BCG_API int bcg_gemm_pp(int epi, const void* x, const void* w, const void* bias, const void* residual, void* c,
+                        void* ws, void* counters, int M, int N, int K, int inter, int split_k, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || N % 16 || K % PBK || K <= 0 || split_k < 1 || K / PBK < split_k) return -2;
+  if (split_k > 1 && (!ws || !counters)) return -2;
+  float* wsf = static_cast<float*>(ws);
+  int* cnt = static_cast<int*>(counters);
+  switch (epi) {
+    case EPI_STORE: return launch_pp<EPI_STORE>(x, w, bias, residual, c, wsf, cnt, M, N, K, inter, split_k, stream);
+    case EPI_SILU_MUL:
+      if (N != 2 * inter || inter % 128) return -2;
+      return launch_pp<EPI_SILU_MUL>(x, w, nullptr, nullptr, c, wsf, cnt, M, N, K, inter, split_k, stream);
+    case EPI_RESIDUAL:
+      if (!residual) return -2;
+      return launch_pp<EPI_RESIDUAL>(x, w, bias, residual, c, wsf, cnt, M, N, K, inter, split_k, stream);
+    default: return -2;
+  }
+}

@@ -27,7 +27,7 @@ def _close(a, b, tol=2e-2):
     assert err <= tol * max(1.0, scale), (err, scale)
 
 
-@pytest.mark.parametrize("cfg", list(range(10)))
+@pytest.mark.parametrize("cfg", list(range(11)))
 @pytest.mark.parametrize("M,N,K", [(37, 256, 512), (200, 768, 1024), (448, 1280, 5120), (1, 256, 128)])
 def test_gemm_store_bias(hip, cfg, M, N, K):
     torch.manual_seed(M + N + cfg)
@@ -42,7 +42,7 @@ def test_gemm_store_bias(hip, cfg, M, N, K):
     _close(yb, _ref(x, w) + b.float())
 
 
-@pytest.mark.parametrize("cfg", list(range(10)))
+@pytest.mark.parametrize("cfg", list(range(11)))
 @pytest.mark.parametrize("M,I,K", [(45, 256, 512), (300, 1024, 1024)])
 def test_gemm_silu_mul_epilogue(hip, cfg, M, I, K):
     torch.manual_seed(I + cfg)
@@ -57,7 +57,7 @@ def test_gemm_silu_mul_epilogue(hip, cfg, M, I, K):
     _close(h, ref)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 3, 10])
 def test_gemm_residual_epilogue_in_place(hip, cfg):
     torch.manual_seed(cfg)
     M, N, K = 77, 512, 2048
@@ -70,7 +70,8 @@ def test_gemm_residual_epilogue_in_place(hip, cfg):
     _close(r, ref)
 
 
-@pytest.mark.parametrize("cfg,split", [(0, 2), (5, 3), (6, 4), (2, 8), (1, 6), (7, 2), (9, 3)])
+@pytest.mark.parametrize("cfg,split", [(0, 2), (5, 3), (6, 4), (2, 8), (1, 6), (7, 2), (9, 3), (10, 2), (10, 3),
+                                       (10, 5)])
 @pytest.mark.parametrize("epi", [0, 1, 2])
 def test_gemm_split_k(hip, cfg, split, epi):
     """Split-K with the in-kernel last-arriver reduction, repeated launches (the counters
@@ -105,3 +106,36 @@ def test_fused_ops_match_unfused(hip):
     _close(h, hip.silu_mul(torch.nn.functional.linear(x, wgu)), 3e-2)
     ref = r.float() + _ref(h, wd)
     _close(hip.linear_residual(h, wd, r.clone()), ref, 3e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 1040, 64), (257, 528, 128), (513, 784, 192), (1, 4112, 320),
+                                   (768, 2048, 1024)])
+@pytest.mark.parametrize("epi", [0, 2])
+def test_gemm_pp_edges(hip, M, N, K, epi):
+    """The 256x256 ping-pong kernel (cfg 10) at its edges: 1-3 K-tiles (prologue-only
+    pipelines), M and N not multiples of the tile (clamped loads, masked stores: the LM head
+    has N = 151936 = 593.5 tiles), repeated launches."""
+    torch.manual_seed(M * 7 + N + K)
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
+    ref = _ref(x, w)
+    for _ in range(2):
+        if epi == 2:
+            r = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+            want = r.float() + ref
+            got = hip.gemm_nt(x, w, 10, 2, residual=r, out=r)
+        else:
+            want = ref
+            got = hip.gemm_nt(x, w, 10, 0)
+        _close(got, want)
+
+
+def test_gemm_pp_prefill_chunk_silu(hip):
+    """A prefill-sized gate_up chunk through the ping-pong kernel with the fused SiLU*mul."""
+    torch.manual_seed(5)
+    M, I, K = 2048 + 77, 1408, 2048
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(2 * I, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
+    gu = _ref(x, w)
+    ref = torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]
+    _close(hip.gemm_nt(x, w, 10, 1), ref)

@@ -27,7 +27,7 @@ import torch.nn.functional as F  # noqa: E402
 
 from byzantine_consensus_llm_agents_amd.models.config import ALIASES, get_model_config  # noqa: E402
 from byzantine_consensus_llm_agents_amd.ops import get_ops  # noqa: E402
-from byzantine_consensus_llm_agents_amd.ops.gemm_plan import N_CFGS, SPLITS, TABLE  # noqa: E402
+from byzantine_consensus_llm_agents_amd.ops.gemm_plan import N_CFGS, PP_CFG, SPLITS, TABLE  # noqa: E402
 
 
 def shapes(cfg, tp):
@@ -87,6 +87,8 @@ def main():
         ws = [torch.randn(N, K, device="cuda", generator=gen).mul_(K ** -0.5).to(torch.bfloat16)
               for _ in range(min(copies, 8))]
         for M in Ms:
+            if M > 1024 and proj == "lm_head":  # prefill computes logits of the last tokens only
+                continue
             x = torch.randn(M, K, device="cuda", generator=gen).to(torch.bfloat16)
             r = torch.randn(M, N, device="cuda", generator=gen).to(torch.bfloat16) if epi == 2 else None
             it = [0]
@@ -109,9 +111,13 @@ def main():
                 lib()
             res["lib"] = timed(lib, args.reps)
             for c in range(N_CFGS):
+                if M > 1024 and c != PP_CFG:  # prefill chunks: the 256x256 kernel or the library
+                    continue
                 bm, bn = hip.gemm_plan.tiles[c]
-                tiles = -(-M // bm) * (N // bn) if N % bn == 0 else 0
+                tiles = -(-M // bm) * -(-N // bn)
                 for sk in SPLITS:
+                    if M > 1024 and sk > 1:
+                        continue
                     if not hip.gemm_plan.supported(c, M, N, K, epi, sk):
                         continue
                     # split-K: fill the rounds of 256 workgroups; never more than ~8 rounds
