@@ -203,6 +203,9 @@ class InferenceEngine:
         # collectives of one communicator must not run on two streams at once.
         self.overlap = bool(args.overlap_prefill and self.device.type == "cuda" and self.tp.size == 1)
         self.prefill_stream = torch.cuda.Stream(self.device) if self.overlap else None
+        if self.overlap and hasattr(self.ops, "gemm_plan"):
+            # no stream-K library GEMM may run beside the other stream's kernels (ops/gemm_plan.py)
+            self.ops.gemm_plan.avoid_library = True
         self._inflight = None
         self._bursts = 0         # decode bursts launched (admission-batching clock)
         self._snap = None        # host copy of (done, gen_count, out_tokens) after the last burst

@@ -11,6 +11,14 @@ simple rule (hand kernel up to ``max_m`` rows).
 
 ``BCG_HAND_GEMM``: ``0`` = library only, ``1`` (default) = table / rule,
 ``force`` = hand kernel wherever the shape is supported (tests).
+
+``avoid_library`` (set by the engine when prefill overlaps decode on a second
+stream): every supported shape runs a hand kernel -- the fastest measured hand
+configuration, else the 256x256 kernel.  hipBLASLt's stream-K kernels (``SK3``,
+picked for the wide decode GEMMs) make workgroups wait for partial tiles of
+other workgroups of the same launch; two such launches on two streams can each
+hold CUs the other's waiting workgroups need (PERF.md, "Overlapped prefill").
+The hand kernels never wait on another workgroup (split-K: last arriver reduces).
 """
 
 import ctypes
@@ -31,6 +39,8 @@ class GemmPlan:
     def __init__(self, lib=None, table: Optional[str] = TABLE, max_m: int = 1024):
         self.mode = os.environ.get("BCG_HAND_GEMM", "1")
         self.max_m = max_m
+        self.avoid_library = False
+        self.timings: Dict[Tuple[int, int, int, int], Dict[str, float]] = {}
         self.tiles = {}
         for cfg in range(N_CFGS):
             self.tiles[cfg] = TILES[cfg]
@@ -41,16 +51,20 @@ class GemmPlan:
         self.table: Dict[Tuple[int, int, int, int], Tuple[int, int]] = {}
         if table and os.path.exists(table):
             with open(table) as fh:
-                for key, choice in json.load(fh).get("choice", {}).items():
-                    m, n, k, e = map(int, key.split(","))
-                    self.table[(m, n, k, e)] = tuple(choice) if isinstance(choice, list) else (int(choice), 1)
+                data = json.load(fh)
+            for key, choice in data.get("choice", {}).items():
+                m, n, k, e = map(int, key.split(","))
+                self.table[(m, n, k, e)] = tuple(choice) if isinstance(choice, list) else (int(choice), 1)
+            for key, times in data.get("timings_us", {}).items():
+                self.timings[tuple(map(int, key.split(",")))] = times
 
     def supported(self, cfg: int, M: int, N: int, K: int, epi: int, split_k: int = 1) -> bool:
         if cfg not in self.tiles or M <= 0 or K % 64 or K <= 0 or split_k < 1 or K // 64 < split_k:
             return False
         bn = self.tiles[cfg][1]
-        if cfg == PP_CFG:
-            return N % 16 == 0 and (epi != 1 or (N % 2 == 0 and (N // 2) % 128 == 0))
+        if cfg == PP_CFG:  # 32-bit buffer offsets: operands below 4 GiB
+            return (N % 16 == 0 and 2 * M * K < 1 << 32 and 2 * N * K < 1 << 32
+                    and (epi != 1 or (N % 2 == 0 and (N // 2) % 128 == 0)))
         if N % bn:
             return False
         if epi == 1 and (N % 2 or (N // 2) % (bn // 2)):
@@ -60,10 +74,26 @@ class GemmPlan:
     def default_cfg(self, M: int) -> int:
         return 1 if M <= 64 else 0
 
+    def _best_hand(self, M: int, N: int, K: int, epi: int) -> Optional[Tuple[int, int]]:
+        """Fastest measured hand configuration of the nearest measured M >= M, else the 256x256 kernel."""
+        above = [m for (m, n, k, e) in self.timings if (n, k, e) == (N, K, epi) and m >= M]
+        if above:
+            times = self.timings[(min(above), N, K, epi)]
+            for name, _ in sorted(((n_, t) for n_, t in times.items() if n_ != "lib" and t), key=lambda kv: kv[1]):
+                cfg, split = map(int, name.split("x"))
+                if self.supported(cfg, M, N, K, epi, split):
+                    return (cfg, split)
+        if self.supported(PP_CFG, M, N, K, epi):
+            return (PP_CFG, 1)
+        cfg = self.default_cfg(M)
+        return (cfg, 1) if self.supported(cfg, M, N, K, epi) else None
+
     def choose(self, M: int, N: int, K: int, epi: int) -> Optional[Tuple[int, int]]:
         """(tile configuration, split-K) of the hand kernel, or None for the library path."""
         if self.mode == "0":
             return None
+        if self.avoid_library:
+            return self._best_hand(M, N, K, epi)
         if self.mode == "force":
             for cfg in (self.default_cfg(M),) + tuple(range(N_CFGS)):
                 if self.supported(cfg, M, N, K, epi):

@@ -43,6 +43,24 @@
 //     (as gemm.hip, cdna_hip_programming.md §6 Guideline 16 R1).
 #include "common.h"
 
+#ifndef PP_GLDS_IN_MFMA
+#define PP_GLDS_IN_MFMA 1  // issue a phase's two glds pieces between its own MFMAs (+5-9 % over the read turn)
+#endif
+#ifndef PP_BUFFER_LDS
+#define PP_BUFFER_LDS 0  // 1: buffer_load ... lds (MUBUF, k offset in soffset): measured 1-3 % slower
+#endif
+#ifndef PP_PIECE0
+#define PP_PIECE0 3  // MFMA index (0..15) after which the phase's first glds piece is issued
+#endif
+#ifndef PP_PIECE1
+#define PP_PIECE1 11
+#endif
+#ifndef PP_RING
+#define PP_RING 10  // 16-KiB half slots in the LDS ring (10 = the whole 160 KiB)
+#endif
+#ifndef PP_LEAD
+#define PP_LEAD (PP_RING - 1)  // a half-tile is loaded PP_LEAD phases before the phase after its read
+#endif
 #ifndef PP_GROUP_M
 #define PP_GROUP_M 8  // m-tiles per tile-order group (L2 reuse of both operands at prefill M)
 #endif
@@ -51,8 +69,15 @@ namespace {
 
 constexpr int PBM = 256, PBN = 256, PBK = 64;
 constexpr int HALF = 128 * 128;  // one half slot: 128 rows x 128 B
-constexpr int BUF = 4 * HALF;    // one K-tile: A-lo, B-lo, B-hi, A-hi
-enum { S_ALO = 0, S_BLO = 1, S_BHI = 2, S_AHI = 3 };
+// half-tile n = 4 t + kind of K-tile t; kind: A-lo, B-lo, B-hi, A-hi.  Half-tile n is read in
+// phase n - 1 (j0: B-lo(t), j1: B-hi(t), j2: A-hi(t), j3: A-lo(t+1)), loaded in phase n - LEAD
+// into ring slot n % RING.  A wait before phase r's first barrier covers the loads of phases
+// <= r - DEPTH; a load of phase p is then visible to the readers of phase >= p + DEPTH + 1
+// (RAW: DEPTH <= LEAD - 2), and a slot is refilled >= 2 phases after its last read (WAR:
+// RING >= LEAD + 1).
+enum { K_ALO = 0, K_BLO = 1, K_BHI = 2, K_AHI = 3 };
+constexpr int RING = PP_RING, LEAD = PP_LEAD, DEPTH = LEAD - 2;
+static_assert(RING >= LEAD + 1 && DEPTH >= 2 && 2 * DEPTH <= 62 && RING * HALF <= 160 * 1024, "ring geometry");
 enum Epilogue { EPI_STORE = 0, EPI_SILU_MUL = 1, EPI_RESIDUAL = 2 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
@@ -78,7 +103,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     int split_k) {
   // ONE shared array (a second __shared__ object can make hipcc drain vmcnt before every
   // ds_read: cdna_hip_programming.md "Projection GEMM" item 4a)
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[RING * HALF];
 
   // ---- XCD-aware order: bijective remap, then (n-tile, m-tile, k-split) ----
   const int nwg = m_tiles * n_tiles * split_k;
@@ -128,16 +153,32 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
       offB[hi][i] = static_cast<uint32_t>(bn) * K + c * 8;
     }
   }
-  auto load_half = [&](int t, int slot) {  // K-tile t (relative) -> buffer t & 1, half `slot`
+  const int nhalf = 4 * nk;  // half-tiles of this workgroup's K range
+  // buffer descriptors (byte ranges < 4 GiB: checked by the host wrapper)
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(X), 0,
+                                                                       static_cast<uint32_t>(M) * K * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(W), 0, static_cast<uint32_t>(EPI == EPI_SILU_MUL ? 2 * inter : N) * K * 2, 0x00020000);
+  // glds piece i of half-tile n (kind = n & 3, K-tile n >> 2) into ring slot `slot`
+  auto load_piece = [&](int n, int kind, int slot, int i) {
 #ifdef PP_ABL_NOLOAD
-    if (t >= 2) return;
+    if (n >= 8) return;
 #endif
-    unsigned char* dst = smem + (t & 1) * BUF + slot * HALF + wave * 2048;
-    const uint32_t k0 = (kt0 + t) * PBK;
-    const bf16_t* base = (slot == S_ALO || slot == S_AHI) ? X : W;
-    const uint32_t* off = slot == S_ALO ? offA[0] : slot == S_AHI ? offA[1] : slot == S_BLO ? offB[0] : offB[1];
-    __builtin_amdgcn_global_load_lds(base + (off[0] + k0), dst, 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(base + (off[1] + k0), dst + 1024, 16, 0, 0);
+    unsigned char* dst = smem + slot * HALF + wave * 2048 + i * 1024;
+    const uint32_t k0 = (kt0 + (n >> 2)) * PBK;
+    const uint32_t* off = kind == K_ALO ? offA[0] : kind == K_AHI ? offA[1] : kind == K_BLO ? offB[0] : offB[1];
+    if constexpr (PP_BUFFER_LDS) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds((kind == K_ALO || kind == K_AHI) ? rsX : rsW,
+                                               (__attribute__((address_space(3))) void*)dst, 16, off[i] * 2, k0 * 2,
+                                               0, 0);
+    } else {
+      const bf16_t* base = (kind == K_ALO || kind == K_AHI) ? X : W;
+      __builtin_amdgcn_global_load_lds(base + (off[i] + k0), dst, 16, 0, 0);
+    }
+  };
+  auto load_half = [&](int n, int kind, int slot) {
+    load_piece(n, kind, slot, 0);
+    load_piece(n, kind, slot, 1);
   };
 
   f32x4 acc[4][8];  // [n-block][m-block]
@@ -153,7 +194,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
 #ifdef PP_ABL_NOREAD
     if (t >= 1) return;
 #endif
-    const unsigned char* base = smem + (t & 1) * BUF + slot * HALF;
+    const unsigned char* base = smem + slot * HALF;
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
@@ -166,7 +207,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
 #ifdef PP_ABL_NOREAD
     if (t >= 1) return;
 #endif
-    const unsigned char* base = smem + (t & 1) * BUF + slot * HALF;
+    const unsigned char* base = smem + slot * HALF;
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
@@ -175,7 +216,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
         b[nb][s] = *reinterpret_cast<const bf16x8*>(base + r * 128 + swz(r, 4 * s + fq) * 16);
       }
   };
-  auto mfma = [&](int nh, int mh, const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2]) {
+  // 16 MFMAs of one quadrant; with PP_GLDS_IN_MFMA the phase's two glds pieces (K-tile lt,
+  // half lslot; lt < 0: none) go between them, where the wave waits on the MFMA pipe anyway
+  auto mfma = [&](int nh, int mh, const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2], int ln, int lkind,
+                  int lslot) {
 #ifndef PP_NO_SETPRIO
     __builtin_amdgcn_s_setprio(1);
 #endif
@@ -184,67 +228,87 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
+        for (int mb = 0; mb < 4; ++mb) {
           acc[nh * 2 + nb][mh * 4 + mb] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nb][s], a[mb][s], acc[nh * 2 + nb][mh * 4 + mb], 0, 0, 0);
+          if constexpr (PP_GLDS_IN_MFMA) {
+            const int idx = (s * 2 + nb) * 4 + mb;
+            if (idx == PP_PIECE0 || idx == PP_PIECE1) {
+              __builtin_amdgcn_sched_barrier(0);
+              if (ln >= 0) load_piece(ln, lkind, lslot, idx == PP_PIECE1);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+        }
 #ifndef PP_NO_SETPRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
   };
-  // counted wait before the phase's first barrier: loads of phases <= p-4 landed
+  // counted wait before the phase's first barrier: loads of phases <= r - DEPTH landed.
+  // Loads issued in the read turn (before the wait): 2*DEPTH younger glds may be in flight;
+  // loads issued among the MFMAs (after the wait): the newest are phase r-1's, 2*(DEPTH-1).
   auto vm_wait = [&](bool full_window) {
     if (full_window) {
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      if constexpr (PP_GLDS_IN_MFMA) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (DEPTH - 1)) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DEPTH) : "memory");
+      }
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   };
-  auto mma_block = [&](int nh, int mh, const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2]) {
+  // one phase: [read turn done by the caller] wait, barrier, MFMAs (+ this phase's load), barrier
+  auto phase = [&](bool window, int nh, int mh, const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2], int ln,
+                   int lkind, int lslot) {
+    if constexpr (!PP_GLDS_IN_MFMA) {
+      if (ln >= 0) load_half(ln, lkind, lslot);
+    }
+    vm_wait(window);
     sbar();  // pre-barrier
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    mfma(nh, mh, a, b);
+    mfma(nh, mh, a, b, PP_GLDS_IN_MFMA ? ln : -1, lkind, lslot);
     sbar();  // post-barrier
   };
 
-  // ---- prologue: phases -6..-1 ----
-  load_half(0, S_ALO);
-  load_half(0, S_BLO);
-  load_half(0, S_BHI);
-  load_half(0, S_AHI);
-  if (nk > 1) {
-    load_half(1, S_ALO);
-    load_half(1, S_BLO);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A-lo(0), B-lo(0) landed
+  // ---- prologue: half-tiles 0..LEAD-1 (phases -LEAD..-1) ----
+#pragma unroll
+  for (int n = 0; n < LEAD; ++n)
+    if (n < nhalf) load_half(n, n & 3, n);  // slot n (n < LEAD < RING)
+  if (nhalf >= LEAD) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (LEAD - 2)) : "memory");  // half-tiles 0, 1 landed
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   sbar();
   if (g == 1) sbar();  // group 1 runs one barrier behind group 0
-  read_a(0, S_ALO, alo);  // phase j3 of "tile -1"
+  read_a(0, 0, alo);   // A-lo(0) = half-tile 0, slot 0 ("phase -1")
 
+  int ls = LEAD % RING, rs = 1;  // ring slots of the next load (n = p + LEAD) and read (n = p + 1)
+  auto bump = [](int& x) { x = x + 1 == RING ? 0 : x + 1; };
   for (int t = 0; t < nk; ++t) {
-    const bool l1 = t + 1 < nk, l2 = t + 2 < nk;
-    // j0: B-lo; load B-hi(t+1)
-    read_b(t, S_BLO, blo);
-    if (l1) load_half(t + 1, S_BHI);
-    vm_wait(l1);
-    mma_block(0, 0, alo, blo);
-    // j1: B-hi; load A-hi(t+1)
-    read_b(t, S_BHI, bhi);
-    if (l1) load_half(t + 1, S_AHI);
-    vm_wait(l1);
-    mma_block(1, 0, alo, bhi);
-    // j2: A-hi; load A-lo(t+2)
-    read_a(t, S_AHI, ahi);
-    if (l2) load_half(t + 2, S_ALO);
-    vm_wait(l2);
-    mma_block(1, 1, ahi, bhi);
-    // j3: A-lo(t+1) (loaded in phase 4t-2: visible from phase 4t+3); load B-lo(t+2)
-    if (l1) read_a(t + 1, S_ALO, alo);
-    if (l2) load_half(t + 2, S_BLO);
-    vm_wait(l2);
-    mma_block(0, 1, ahi, blo);
+    const int p0 = 4 * t;
+    // phase p loads half-tile p + LEAD (if any); kinds are compile-time per j
+    auto ln = [&](int j) { return p0 + j + LEAD < nhalf ? p0 + j + LEAD : -1; };
+    // wait windows: read-turn loads -> phase r has a load; loads among MFMAs -> phase r-1 has one
+    auto win = [&](int j) { return (p0 + j + LEAD - (PP_GLDS_IN_MFMA ? 1 : 0)) < nhalf; };
+    // j0: read B-lo(t)
+    read_b(t, rs, blo);
+    phase(win(0), 0, 0, alo, blo, ln(0), (0 + LEAD) & 3, ls);
+    bump(ls), bump(rs);
+    // j1: read B-hi(t)
+    read_b(t, rs, bhi);
+    phase(win(1), 1, 0, alo, bhi, ln(1), (1 + LEAD) & 3, ls);
+    bump(ls), bump(rs);
+    // j2: read A-hi(t)
+    read_a(t, rs, ahi);
+    phase(win(2), 1, 1, ahi, bhi, ln(2), (2 + LEAD) & 3, ls);
+    bump(ls), bump(rs);
+    // j3: read A-lo(t+1)
+    if (t + 1 < nk) read_a(t + 1, rs, alo);
+    phase(win(3), 0, 1, ahi, blo, ln(3), (3 + LEAD) & 3, ls);
+    bump(ls), bump(rs);
   }
   if (g == 0) sbar();  // balance group 1's extra barrier
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -347,6 +411,7 @@ int launch_pp(const void* x, const void* w, const void* bias, const void* res, v
 BCG_API int bcg_gemm_pp(int epi, const void* x, const void* w, const void* bias, const void* residual, void* c,
                         void* ws, void* counters, int M, int N, int K, int inter, int split_k, hipStream_t stream) {
   if (M <= 0 || N <= 0 || N % 16 || K % PBK || K <= 0 || split_k < 1 || K / PBK < split_k) return -2;
+  if (2ull * M * K >= (1ull << 32) || 2ull * N * K >= (1ull << 32)) return -2;  // 32-bit buffer offsets
   if (split_k > 1 && (!ws || !counters)) return -2;
   float* wsf = static_cast<float*>(ws);
   int* cnt = static_cast<int*>(counters);

@@ -1,0 +1,46 @@
+"""GEMM dispatch plan (ops/gemm_plan.py) on the CPU: table lookups, the 256x256 kernel's
+shape rules, and the no-library mode the overlapped-prefill engine relies on."""
+import json
+
+from byzantine_consensus_llm_agents_amd.ops.gemm_plan import PP_CFG, GemmPlan
+
+
+def _plan(tmp_path, choice, timings):
+    path = tmp_path / "t.json"
+    path.write_text(json.dumps({"choice": choice, "timings_us": timings}))
+    return GemmPlan(lib=None, table=str(path))
+
+
+def test_table_and_nearest_bucket(tmp_path, monkeypatch):
+    monkeypatch.setenv("BCG_HAND_GEMM", "1")
+    p = _plan(tmp_path, {"448,5120,5120,2": [9, 1], "768,5120,5120,2": [-1, 1], "16384,34816,5120,1": [10, 1]},
+              {})
+    assert p.choose(448, 5120, 5120, 2) == (9, 1)
+    assert p.choose(430, 5120, 5120, 2) == (9, 1)          # nearest measured M above
+    assert p.choose(700, 5120, 5120, 2) is None             # library measured faster
+    assert p.choose(9000, 34816, 5120, 1) == (PP_CFG, 1)    # prefill chunk -> 16384 entry
+    assert p.choose(20000, 34816, 5120, 1) is None          # nothing measured above: library
+
+
+def test_pp_shape_rules(monkeypatch):
+    monkeypatch.setenv("BCG_HAND_GEMM", "1")
+    p = GemmPlan(lib=None, table=None)
+    assert p.supported(PP_CFG, 768, 151936, 5120, 0)       # LM head: N = 593.5 tiles, masked tail
+    assert not p.supported(PP_CFG, 768, 151930, 5120, 0)   # N % 16
+    assert not p.supported(PP_CFG, 768, 1000, 5120, 1)     # silu: inter % 128
+    assert p.supported(PP_CFG, 768, 2 * 17408, 5120, 1)
+    assert not p.supported(PP_CFG, 300000, 8192, 8192, 0)  # X beyond 4 GiB (32-bit buffer offsets)
+    assert not p.supported(PP_CFG, 64, 256, 100, 0)        # K % 64
+
+
+def test_avoid_library_picks_fastest_hand_config(tmp_path, monkeypatch):
+    """Overlapped prefill: a shape whose table entry is the library must still get a hand kernel
+    (the fastest measured hand configuration, else the 256x256 kernel)."""
+    monkeypatch.setenv("BCG_HAND_GEMM", "1")
+    p = _plan(tmp_path, {"768,34816,5120,1": [-1, 1]},
+              {"768,34816,5120,1": {"lib": 290.0, "8x1": 345.0, "10x1": 300.0, "7x1": 350.0}})
+    assert p.choose(768, 34816, 5120, 1) is None
+    p.avoid_library = True
+    assert p.choose(768, 34816, 5120, 1) == (10, 1)
+    assert p.choose(16384, 5120, 17408, 2) == (PP_CFG, 1)  # unmeasured: the 256x256 kernel
+    assert p.choose(5, 4096, 4096, 0) is not None

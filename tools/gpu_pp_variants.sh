@@ -9,18 +9,17 @@ for v in ${VARIANTS:-$(ls build | grep '^pp_' | sed 's/^pp_//')}; do
     timeout -k 5 60 build/pp_$v ${s//,/ } 30 || { echo "variant $v shape $s failed"; exit 1; }
   done
 done | tee gpurun_out/ppv/times.jsonl
-[ -z "$PMC_VARIANT" ] && exit 0
+[ -z "$PMC_VARIANTS" ] && exit 0
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-i=0
-while read -r group; do
-  [ -z "$group" ] && continue
-  i=$((i+1))
-  timeout -s KILL 60 rocprofv3 --pmc $group --output-format csv -d gpurun_out/ppv/p$i -o run -- \
-    build/pp_$PMC_VARIANT ${PMC_SHAPE//,/ } 10 > gpurun_out/ppv/p$i.log 2>&1 || { echo "pass $i failed: $group"; tail -3 gpurun_out/ppv/p$i.log; exit 1; }
-  echo "pass $i ok: $group"
-done <<GROUPS
-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES
-SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE
-FETCH_SIZE TCC_HIT_sum
-GROUPS
-python tools/pmc_summary.py gpurun_out/ppv | tee gpurun_out/ppv/summary.txt
+GROUPS_TXT=${PMC_GROUPS:-"SQ_WAVES,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_INSTS_MFMA,SQ_VALU_MFMA_BUSY_CYCLES;SQ_INSTS_LDS,SQ_LDS_BANK_CONFLICT,SQ_ACTIVE_INST_LDS,SQ_WAIT_INST_LDS,SQ_INST_CYCLES_VMEM,GRBM_GUI_ACTIVE;FETCH_SIZE,TCC_HIT_sum"}
+for v in $PMC_VARIANTS; do
+  i=0
+  IFS=';' read -ra GROUPS_ARR <<< "$GROUPS_TXT"
+  for group in "${GROUPS_ARR[@]}"; do
+    i=$((i+1))
+    timeout -s KILL 60 rocprofv3 --pmc ${group//,/ } --output-format csv -d gpurun_out/ppv/$v/p$i -o run -- \
+      build/pp_$v ${PMC_SHAPE//,/ } 10 > gpurun_out/ppv/$v.p$i.log 2>&1 || { echo "pass $v/$i failed: $group"; tail -3 gpurun_out/ppv/$v.p$i.log; exit 1; }
+    echo "pass $v/$i ok: $group"
+  done
+  echo "== $v"; python tools/pmc_summary.py gpurun_out/ppv/$v | grep -A40 gemm_pp | tee gpurun_out/ppv/summary_$v.txt
+done

@@ -58,7 +58,10 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--merge", action="store_true", help="add to the existing table instead of replacing it")
     ap.add_argument("--skip", default="", help="comma list of projections to skip")
+    ap.add_argument("--cfgs", default="", help="comma list of tile configurations to time (default: all); "
+                    "with --merge the table's previous best configuration is timed again as well")
     args = ap.parse_args()
+    only_cfgs = {int(c) for c in args.cfgs.split(",") if c}
     os.environ["BCG_HAND_GEMM"] = "0"  # the library path of linear() must not dispatch to us
     hip = get_ops("hip")
     name = ALIASES.get(args.model, args.model).split("/")[-1].lower()
@@ -110,13 +113,19 @@ def main():
             for _ in range(3):
                 lib()
             res["lib"] = timed(lib, args.reps)
+            key = f"{M},{N},{K},{epi}"
+            prev = table["choice"].get(key) if args.merge else None
             for c in range(N_CFGS):
                 if M > 1024 and c != PP_CFG:  # prefill chunks: the 256x256 kernel or the library
+                    continue
+                if only_cfgs and c not in only_cfgs and not (prev and prev[0] == c):
                     continue
                 bm, bn = hip.gemm_plan.tiles[c]
                 tiles = -(-M // bm) * -(-N // bn)
                 for sk in SPLITS:
                     if M > 1024 and sk > 1:
+                        continue
+                    if only_cfgs and c not in only_cfgs and [c, sk] != list(prev):
                         continue
                     if not hip.gemm_plan.supported(c, M, N, K, epi, sk):
                         continue
@@ -140,7 +149,6 @@ def main():
                         fn()
                     res[(c, sk)] = timed(fn, args.reps)
             best = min(res, key=lambda k: res[k] if res[k] is not None else 1e30)
-            key = f"{M},{N},{K},{epi}"
             table["choice"][key] = [-1, 1] if best == "lib" else list(best)
             table["timings_us"][key] = {(k if k == "lib" else f"{k[0]}x{k[1]}"): round(v, 2) for k, v in res.items()}
             hand = min((v for k, v in res.items() if k != "lib"), default=None)
