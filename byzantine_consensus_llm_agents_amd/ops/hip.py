@@ -24,7 +24,7 @@ def load_library(path: str = None) -> ctypes.CDLL:
     global _LIB
     if _LIB is not None:
         return _LIB
-    path = path or kernels_target()
+    path = path or os.environ.get("BCG_KERNELS_LIB") or kernels_target()  # override: variant builds (tools)
     if not os.path.exists(path):
         raise RuntimeError(f"HIP kernel library not found at {path}; run `python -m "
                            "byzantine_consensus_llm_agents_amd.utils.build` (hipcc --offload-arch=gfx950)")

@@ -413,8 +413,19 @@ void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
 // K/V once for all of them: every 16-B K/V load feeds NT times the MFMAs of
 // the one-tile (NT = 1) form, which was load-bound (L2 -> CU) at 120-200 TF/s.
 // Waves of a block: 4/NT row groups x NT heads; grid = (tiles, ceil(n_q/NT)).
+#ifndef PREFILL_LAZY
+#define PREFILL_LAZY true
+#endif
+#ifndef PREFILL_WPE
+#define PREFILL_WPE 0
+#endif
+#if PREFILL_WPE
+#define PREFILL_ATTR __attribute__((amdgpu_waves_per_eu(1, 1)))
+#else
+#define PREFILL_ATTR
+#endif
 template <int HD, int NT, bool F8 = false>
-__global__ __launch_bounds__(256) void prefill_attn_kernel(
+__global__ __launch_bounds__(256) PREFILL_ATTR void prefill_attn_kernel(
     const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
     const int* __restrict__ q_start, const int* __restrict__ seq_lens, const int* __restrict__ tiles,
     int n_q, float scale_log2, bf16_t* __restrict__ out) {
@@ -477,11 +488,11 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
     for (int nt = 0; nt < NT; ++nt) {
       if (c * CHUNK >= sub_end[nt]) continue;  // wave-uniform: chunk wholly in this sub-tile's causal future
       if ((c + 1) * CHUNK <= sub_first[nt])     // wave-uniform: every key visible to every row
-        compute_chunk<HD, Causal, false, F8, false>(cur, bq[nt], c * CHUNK, sub_end[nt], Causal{my_pos[nt]},
-                                                    scale_log2, m[nt], l[nt], o[nt], lane);
+        compute_chunk<HD, Causal, false, F8, PREFILL_LAZY>(cur, bq[nt], c * CHUNK, sub_end[nt], Causal{my_pos[nt]},
+                                                           scale_log2, m[nt], l[nt], o[nt], lane);
       else
-        compute_chunk<HD, Causal, true, F8, false>(cur, bq[nt], c * CHUNK, sub_end[nt], Causal{my_pos[nt]},
-                                                   scale_log2, m[nt], l[nt], o[nt], lane);
+        compute_chunk<HD, Causal, true, F8, PREFILL_LAZY>(cur, bq[nt], c * CHUNK, sub_end[nt], Causal{my_pos[nt]},
+                                                          scale_log2, m[nt], l[nt], o[nt], lane);
     }
     cur = nxt;
   }

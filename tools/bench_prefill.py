@@ -90,6 +90,7 @@ def main():
     ap.add_argument("--skip-gemm", action="store_true")
     ap.add_argument("--skip-attn", action="store_true")
     ap.add_argument("--attn-model", default=None, help="model geometry for the attention runs")
+    ap.add_argument("--nts", default="0,4", help="prefill kernel forms to time (0 = LDS-staged, 1/2/4 = NT)")
     args = ap.parse_args()
     cfg = get_model_config(args.model)
     out = {"model": cfg.name, "gemm": {}, "attention": []}
@@ -111,7 +112,7 @@ def main():
         torch.backends.cuda.preferred_blas_library("cublaslt")
         torch.cuda.tunable.enable(False)
     acfg = get_model_config(args.attn_model) if args.attn_model else cfg
-    for nt in (() if args.skip_attn else (0, 4)):
+    for nt in (() if args.skip_attn else [int(x) for x in args.nts.split(",")]):
         for n, p, pre in ((12, 1024, 512), (16, 900, 400), (8, 2048, 0)):
             out["attention"].append(attention(acfg, n, p, pre, nt))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
