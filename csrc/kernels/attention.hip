@@ -99,6 +99,37 @@ __device__ __forceinline__ void load_chunk(Chunk<HD, F8>& c, const KVGeom& g, in
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// The K half / V half of load_chunk, for loops that reload a chunk's registers in place
+// (K right after the S^T MFMAs consumed it, V after the P.V MFMAs).
+template <int HD, bool F8 = false>
+__device__ __forceinline__ void load_chunk_k(Chunk<HD, F8>& c, const KVGeom& g, int blk0, int blk1, int kvh,
+                                             int lane) {
+  typedef typename Chunk<HD, F8>::E E;
+  typedef typename std::conditional<F8, uint8_t, bf16_t>::type T;
+  const T* kc = reinterpret_cast<const T*>(g.k);
+  const int r = lane & 15, h = lane >> 4;
+  const size_t b0 = block_base<HD>(g, blk0, kvh), b1 = block_base<HD>(g, blk1, kvh);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int t = 8 * (r >> 2) + 4 * u + (r & 3);
+    const T* krow = kc + (t < BS ? b0 : b1) + (t & (BS - 1)) * HD + 8 * h;
+#pragma unroll
+    for (int kk = 0; kk < HD / 32; ++kk) c.k[u][kk] = *reinterpret_cast<const E*>(krow + kk * 32);
+  }
+}
+
+template <int HD, bool F8 = false>
+__device__ __forceinline__ void load_chunk_v(Chunk<HD, F8>& c, const KVGeom& g, int blk0, int blk1, int kvh,
+                                             int lane) {
+  typedef typename Chunk<HD, F8>::E E;
+  typedef typename std::conditional<F8, uint8_t, bf16_t>::type T;
+  const T* vc = reinterpret_cast<const T*>(g.v);
+  const int r = lane & 15, h = lane >> 4;
+  const T* vb = vc + block_base<HD>(g, h < 2 ? blk0 : blk1, kvh) + 8 * (h & 1);
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt) c.v[dt] = *reinterpret_cast<const E*>(vb + (dt * 16 + r) * BS);
+}
+
 // Reductions over the 4 lane rows (h = lane >> 4) that share a query column:
 // v_permlane16_swap (rows 0<->1, 2<->3) then v_permlane32_swap (0<->2, 1<->3),
 // two VALU ops each instead of ds_bpermute round trips through the LDS
@@ -206,6 +237,69 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16
       o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(to_bf16x8(c.v[dt]), bp, o[dt], 0, 0, 0);
     }
   }
+}
+
+
+// All NT query sub-tiles of a wave on one chunk that every row of every sub-tile sees in
+// full (no mask), as ONE straight-line block: the S^T MFMAs of every sub-tile first, then
+// each sub-tile's softmax (its VALU runs while the later sub-tiles' MFMAs are still in the
+// pipe), then every P.V MFMA.  Lazy rescale with ONE wave-uniform branch for all
+// sub-tiles (taken only when some column's running max moves by > 2^RESCALE_LOG2): the
+// per-sub-tile branches of compute_chunk split the chunk into basic blocks the compiler
+// cannot interleave.
+template <int HD, int NT, bool F8, typename ReloadK, typename ReloadV>
+__device__ __forceinline__ void compute_chunk_full(Chunk<HD, F8>& c, const bf16x8 (&bq)[NT][HD / 32],
+                                                   float scale_log2, float (&m)[NT], float (&l)[NT],
+                                                   f32x4 (&o)[NT][HD / 16], ReloadK reload_k, ReloadV reload_v) {
+  f32x4 s[NT][2];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      s[nt][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < HD / 32; ++kk)
+        s[nt][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(to_bf16x8(c.k[u][kk]), bq[nt][kk], s[nt][u], 0, 0, 0);
+    }
+  reload_k(c);  // next chunk's K into the registers the S^T MFMAs just read
+  float mx[NT];
+  bool grow = false;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    float v = fmaxf(fmaxf(fmaxf(s[nt][0][0], s[nt][0][1]), fmaxf(s[nt][0][2], s[nt][0][3])),
+                    fmaxf(fmaxf(s[nt][1][0], s[nt][1][1]), fmaxf(s[nt][1][2], s[nt][1][3])));
+    mx[nt] = rows_max(v * scale_log2);
+    grow |= mx[nt] > m[nt] + RESCALE_LOG2;
+  }
+  if (__builtin_amdgcn_ballot_w64(grow) != 0) {  // wave-uniform, rare after the first chunks
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const float m_new = fmaxf(m[nt], mx[nt]);
+      const float alpha = m[nt] == -INFINITY ? 0.f : exp2f(m[nt] - m_new);
+      l[nt] *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) o[nt][dt] *= alpha;
+      m[nt] = m_new;
+    }
+  }
+  bf16x8 bp[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    float ps = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float pj = exp2f(s[nt][j >> 2][j & 3] * scale_log2 - m[nt]);
+      ps += pj;
+      bp[nt][j] = static_cast<__bf16>(pj);
+    }
+    l[nt] += rows_sum(ps);
+  }
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt)
+      o[nt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(to_bf16x8(c.v[dt]), bp[nt], o[nt][dt], 0, 0, 0);
+  reload_v(c);
 }
 
 template <int HD>
@@ -414,7 +508,10 @@ void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
 // the one-tile (NT = 1) form, which was load-bound (L2 -> CU) at 120-200 TF/s.
 // Waves of a block: 4/NT row groups x NT heads; grid = (tiles, ceil(n_q/NT)).
 #ifndef PREFILL_LAZY
-#define PREFILL_LAZY true
+#define PREFILL_LAZY false  // measured: see PERF.md (lazy spills at NT = 4)
+#endif
+#ifndef PREFILL_FULL_BLOCK
+#define PREFILL_FULL_BLOCK 0  // 1: fully visible chunks through compute_chunk_full (lazy rescale, in-place reload)
 #endif
 #ifndef PREFILL_WPE
 #define PREFILL_WPE 0
@@ -479,9 +576,26 @@ __global__ __launch_bounds__(256) PREFILL_ATTR void prefill_attn_kernel(
   };
   // next-chunk loads issued unconditionally (clamped to the last chunk) -- see decode
   const int nchunk = (kv_end + CHUNK - 1) / CHUNK;
-  Chunk<HD, F8> cur, nxt;
+  Chunk<HD, F8> cur;
   load_chunk<HD, false, F8>(cur, g, block_at(0), block_at(min(1, nblk - 1)), kvh, lane);
+#if PREFILL_FULL_BLOCK
+  // chunks every row of the wave sees in full: one interleaved block for all NT sub-tiles,
+  // the next chunk reloaded in place (K after the S^T MFMAs, V after the P.V MFMAs): no
+  // second register set for the prefetch
+  int c = 0;
+  for (; (c + 1) * CHUNK <= sub_first[0] && c < nchunk; ++c) {
+    const int cn = min(c + 1, nchunk - 1);
+    const int b0 = block_at(2 * cn), b1 = block_at(min(2 * cn + 1, nblk - 1));
+    compute_chunk_full<HD, NT, F8>(
+        cur, bq, scale_log2, m, l, o, [&](Chunk<HD, F8>& x) { load_chunk_k<HD, F8>(x, g, b0, b1, kvh, lane); },
+        [&](Chunk<HD, F8>& x) { load_chunk_v<HD, F8>(x, g, b0, b1, kvh, lane); });
+  }
+  Chunk<HD, F8> nxt;
+  for (; c < nchunk; ++c) {
+#else
+  Chunk<HD, F8> nxt;
   for (int c = 0; c < nchunk; ++c) {
+#endif
     const int cn = min(c + 1, nchunk - 1);
     load_chunk<HD, false, F8>(nxt, g, block_at(2 * cn), block_at(min(2 * cn + 1, nblk - 1)), kvh, lane);
 #pragma unroll
