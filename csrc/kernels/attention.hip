@@ -511,7 +511,7 @@ void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
 #define PREFILL_LAZY false  // measured: see PERF.md (lazy spills at NT = 4)
 #endif
 #ifndef PREFILL_FULL_BLOCK
-#define PREFILL_FULL_BLOCK 0  // 1: fully visible chunks through compute_chunk_full (lazy rescale, in-place reload)
+#define PREFILL_FULL_BLOCK 1  // fully visible chunks through compute_chunk_full (lazy rescale, in-place reload)
 #endif
 #ifndef PREFILL_WPE
 #define PREFILL_WPE 0
