@@ -586,9 +586,14 @@ __global__ __launch_bounds__(256) PREFILL_ATTR void prefill_attn_kernel(
   for (; (c + 1) * CHUNK <= sub_first[0] && c < nchunk; ++c) {
     const int cn = min(c + 1, nchunk - 1);
     const int b0 = block_at(2 * cn), b1 = block_at(min(2 * cn + 1, nblk - 1));
+#ifdef PREFILL_ABL_NORELOAD  // timing-only ablation: every chunk reuses chunk 0's K/V
+    (void)b0, (void)b1;
+    compute_chunk_full<HD, NT, F8>(cur, bq, scale_log2, m, l, o, [](Chunk<HD, F8>&) {}, [](Chunk<HD, F8>&) {});
+#else
     compute_chunk_full<HD, NT, F8>(
         cur, bq, scale_log2, m, l, o, [&](Chunk<HD, F8>& x) { load_chunk_k<HD, F8>(x, g, b0, b1, kvh, lane); },
         [&](Chunk<HD, F8>& x) { load_chunk_v<HD, F8>(x, g, b0, b1, kvh, lane); });
+#endif
   }
   Chunk<HD, F8> nxt;
   for (; c < nchunk; ++c) {
