@@ -62,6 +62,8 @@ def parse(argv=None):
     ap.add_argument("--honest", type=int, default=8)
     ap.add_argument("--byzantine", type=int, default=2)
     ap.add_argument("--sims-per-gpu", type=int, default=128)
+    ap.add_argument("--max-batch-seqs", type=int, default=None,
+                    help="decode batch cap (rows); default ENGINE_CONFIG['max_batch_seqs']")
     ap.add_argument("--ramp-s", type=float, default=None,
                     help="start the games spread over this many seconds (default: half the warmup)")
     ap.add_argument("--tp", type=int, default=1)
@@ -234,6 +236,8 @@ def main(argv=None):
                            use_hip_graphs=not args.no_graphs, prefix_caching=not args.no_prefix_cache,
                            overlap_prefill=args.overlap_prefill, custom_allreduce=not args.no_custom_allreduce,
                            kv_cache_dtype=args.kv_cache_dtype)
+    if args.max_batch_seqs:
+        C.ENGINE_CONFIG["max_batch_seqs"] = args.max_batch_seqs
     C.BCG_CONFIG["value_range"] = (0, 50)
     random.seed(args.seed + rank)
 

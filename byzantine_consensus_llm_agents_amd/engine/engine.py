@@ -243,7 +243,8 @@ class InferenceEngine:
             free, total = torch.cuda.mem_get_info(self.device)
             # prefill activations of one chunk + the decode graphs' private pool (largest
             # bucket: logits / sampler temporaries, MLP activations) + the shared split-K scratch
-            rows = min(a.max_batch_seqs, 768)
+            from .graphs import MAX_ROWS
+            rows = min(a.max_batch_seqs, MAX_ROWS)
             graphs = rows * (m.cfg.vocab_size * 8 + 8 * m.inter + 16 * m.cfg.hidden_size) * 2
             reserve = (6 * 2 ** 30 + 2 * a.prefill_chunk_tokens * (m.cfg.hidden_size + 2 * m.inter) * 2
                        + graphs + self._decode_ws_bytes())
@@ -675,7 +676,7 @@ class InferenceEngine:
             steps = self.graphs.run_burst(n) if self.graphs is not None else self._eager_burst(n)
         self.stats["decode_steps"] += steps
         self.stats["decode_row_steps"] += steps * len(rows)  # mean live rows = this / decode_steps
-        band = f"rows_le_{min(768, 1 << max(0, (n - 1).bit_length()))}"
+        band = f"rows_le_{1 << max(0, (n - 1).bit_length()) if n <= 512 else (768 if n <= 768 else 1024 if n <= 1024 else 1536)}"
         self.stats[band] = self.stats.get(band, 0) + steps
         self._bursts += 1
 

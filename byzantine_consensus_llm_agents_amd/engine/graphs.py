@@ -21,7 +21,9 @@ import torch
 # 32-row steps above 128: a decode step computes every row of its bucket, so the
 # padding between the live rows and the bucket is wasted GEMM work (~5 % at
 # 32-row steps against ~12 % at the former 64/128-row steps, B ~ 330).
-BUCKETS = (1, 2, 4, 8, 12, 16, 24, 32, 40, 48, 64, 80, 96, 112, 128) + tuple(range(160, 769, 32))
+# Buckets above 768 are captured only when the engine's max_batch_seqs allows them.
+BUCKETS = (1, 2, 4, 8, 12, 16, 24, 32, 40, 48, 64, 80, 96, 112, 128) + tuple(range(160, 1025, 32)) + \
+    tuple(range(1088, 1537, 64))
 MAX_ROWS = BUCKETS[-1]
 
 
