@@ -54,6 +54,8 @@ def load_library(path: str = None) -> ctypes.CDLL:
         "bcg_silu_mul_fp8": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
         "bcg_gemm_nt": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_int, c_int, c_int, c_int, c_int, c_void_p],
+        "bcg_gemm_nt_fp8": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                            c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
         "bcg_gemm_tile": [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)],
         "bcg_gemm_num_cfgs": [],
         "bcg_guided_sample": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -168,7 +170,7 @@ def hip_ops() -> SimpleNamespace:
         _req(q.is_contiguous() and block_tables.dtype == torch.int32 and block_tables.is_contiguous()
              and block_tables.shape[0] == B and seq_lens.numel() == B, "decode attention inputs")
         max_blocks = block_tables.shape[1]
-        _req(B <= 1024, "decode attention: at most 1024 rows")
+        _req(B <= 2048, "decode attention: at most 2048 rows")
         split = lib.bcg_decode_split_tokens(B, n_kv, max_blocks * BS)
         max_splits = (max_blocks * BS + split - 1) // split
         need = B * n_q * max_splits * (hd + 2)
@@ -359,15 +361,67 @@ def hip_ops() -> SimpleNamespace:
         _check(lib.bcg_silu_mul_fp8(_p(gu), _p(q), _p(s), T, I2 // 2, _stream()), "silu_mul_fp8")
         return q, s
 
+    def gemm_nt_fp8(xq, xs, wq, ws, cfg, epi=0, bias=None, residual=None, out=None, split_k=1):
+        """Hand fp8 MFMA GEMM (csrc/kernels/gemm.hip, F8): xs[m] * ws[n] * (xq . wq^T)
+        (+ bias) (+ residual when epi == 2), e4m3fn operands, bf16 out."""
+        if isinstance(cfg, (tuple, list)):
+            cfg, split_k = cfg
+        M, K = xq.shape
+        N = wq.shape[0]
+        _req(xq.dtype == f8 and wq.dtype == f8 and xq.is_contiguous() and wq.is_contiguous() and wq.shape[1] == K,
+             "gemm_nt_fp8: contiguous e4m3fn xq [M,K], wq [N,K]")
+        _req(xs.dtype == torch.float32 and xs.numel() == M and xs.is_contiguous() and ws.dtype == torch.float32
+             and ws.numel() == N and ws.is_contiguous(), "gemm_nt_fp8: fp32 scales xs [M], ws [N]")
+        bm, bn = plan.tiles[cfg]
+        _req(0 <= cfg < 10 and K % 128 == 0 and N % bn == 0 and 1 <= split_k <= K // 128 and epi in (0, 2),
+             f"gemm_nt_fp8: shape {M}x{N}x{K} epi {epi} split {split_k} unsupported by tile {cfg}")
+        if out is None:
+            out = torch.empty(M, N, dtype=torch.bfloat16, device=xq.device)
+        _req(out.shape == (M, N) and out.is_contiguous() and out.dtype == torch.bfloat16, "gemm_nt_fp8: out")
+        if bias is not None:
+            _req(bias.shape == (N,) and bias.dtype == torch.bfloat16 and bias.is_contiguous(), "gemm_nt_fp8: bias")
+        if epi == 2:
+            _req(residual is not None and residual.shape == (M, N) and residual.is_contiguous()
+                 and residual.dtype == torch.bfloat16, "gemm_nt_fp8: residual [M,N] bf16")
+        wsp = cnt = None
+        if split_k > 1:
+            tiles = (M + bm - 1) // bm * (N // bn)
+            _req(tiles <= (1 << 16), "gemm_nt_fp8: too many output tiles for split-K")
+            wsp = torch.empty(tiles * split_k * bm * bn, dtype=torch.float32, device=xq.device)
+            cnt = _counters(xq.device)
+        _check(lib.bcg_gemm_nt_fp8(cfg, epi, _p(xq), _p(wq), _p(xs), _p(ws), _p(bias) if bias is not None else None,
+                                   _p(residual) if residual is not None else None, _p(out),
+                                   _p(wsp) if wsp is not None else None, _p(cnt) if cnt is not None else None,
+                                   M, N, K, split_k, _stream()), "gemm_nt_fp8")
+        return out
+
+    def fp8_cfg(M, N, K):
+        """Tile for the hand fp8 GEMM, or None for hipBLASLt (torch._scaled_mm).  Decode-sized M
+        only: the rule follows the measured choices of tools/bench_fp8_gemm.py."""
+        mode = os.environ.get("BCG_HAND_GEMM", "1")
+        if mode == "0" or K % 128 or M > fp8_hand_max_m:
+            return None
+        for cfg in ((6,) if M <= 32 else (1,) if M <= 64 else (0,) if M <= 128 else (9, 0)):
+            if N % plan.tiles[cfg][1] == 0:
+                return (cfg, 1)
+        return None
+
+    fp8_hand_max_m = int(os.environ.get("BCG_FP8_HAND_MAX_M", "1024"))
+
     def linear_fp8(xq, xs, wq, ws, bias=None, out_dtype=torch.bfloat16):
-        """hipBLASLt fp8 GEMM (torch._scaled_mm) with row-wise activation and weight scales."""
+        """fp8 projection with row-wise activation and per-channel weight scales: the hand
+        fp8 MFMA kernel for decode-sized M, hipBLASLt (torch._scaled_mm) otherwise."""
         _req(xq.dtype == f8 and wq.dtype == f8 and xq.shape[1] == wq.shape[1], "linear_fp8 operands")
+        if out_dtype == torch.bfloat16 and xq.is_contiguous() and wq.is_contiguous():
+            cfg = fp8_cfg(xq.shape[0], wq.shape[0], xq.shape[1])
+            if cfg is not None:
+                return gemm_nt_fp8(xq, xs.contiguous(), wq, ws.contiguous(), cfg, 0, bias=bias)
         return torch._scaled_mm(xq, wq.t(), scale_a=xs.view(-1, 1), scale_b=ws.view(1, -1), bias=bias,
                                 out_dtype=out_dtype)
 
     return SimpleNamespace(name="hip", linear=linear, linear_silu=linear_silu, linear_residual=linear_residual,
                            gemm_nt=gemm_nt, gemm_plan=plan, quant_fp8=quant_fp8, add_rmsnorm_fp8=add_rmsnorm_fp8,
-                           silu_mul_fp8=silu_mul_fp8, linear_fp8=linear_fp8, rmsnorm=rmsnorm, add_rmsnorm=add_rmsnorm, silu_mul=silu_mul,
+                           silu_mul_fp8=silu_mul_fp8, linear_fp8=linear_fp8, gemm_nt_fp8=gemm_nt_fp8, fp8_cfg=fp8_cfg, rmsnorm=rmsnorm, add_rmsnorm=add_rmsnorm, silu_mul=silu_mul,
                            embed_rmsnorm=embed_rmsnorm,
                            qk_norm_rope_kv_write=qk_norm_rope_kv_write,
                            paged_attention_decode=paged_attention_decode,

@@ -332,7 +332,7 @@ struct Causal {
 // the block-table width instead (graph-safe, but ctx << max_model_len) spent
 // most of its workgroups reading seq_lens only to exit: 78 % of the launch at
 // B = 160, ctx 1700, max_model_len 8192.
-constexpr int DEC_MAX_B = 1024;
+constexpr int DEC_MAX_B = 2048;
 
 template <int HD, bool KT = false, bool F8 = false, int CPW = 1>
 __global__ __launch_bounds__(256) void decode_attn_kernel(
@@ -353,10 +353,11 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
 
   // ---- item enumeration: s_pre[b] = sum_{b' < b} ceil(ctx_b' / 128)
   {
-    const int per = (B + 255) / 256;  // <= 4
-    int cnt[4], sum = 0;
+    constexpr int PER_MAX = DEC_MAX_B / 256;
+    const int per = (B + 255) / 256;  // <= PER_MAX
+    int cnt[PER_MAX], sum = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < PER_MAX; ++j) {
       const int i = tid * per + j;
       cnt[j] = (j < per && i < B) ? (seq_lens[i] + DEC_SPLIT - 1) / DEC_SPLIT : 0;
       sum += cnt[j];
@@ -372,7 +373,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
     int base = incl - sum;
     for (int ww = 0; ww < w; ++ww) base += s_wsum[ww];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < PER_MAX; ++j) {
       const int i = tid * per + j;
       if (j < per && i < B) s_pre[i] = base;
       base += cnt[j];
@@ -454,26 +455,57 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   }
 }
 
+// Split merge: one wave per (row, query head), four per workgroup.  Lane s holds split s's
+// (m, l) -- all of them fetched by ONE load instruction, reduced with cross-lane ops --
+// then every split's O partial (HD floats, one coalesced load per split, HD / 64 per lane)
+// is weighted by its factor, broadcast with v_readlane.  The former one-thread-per-dim
+// form walked the splits with dependent broadcast loads twice (35 us per layer at B = 616).
+constexpr int COMBINE_WAVES = 4;
 template <int HD>
-__global__ __launch_bounds__(HD) void decode_combine_kernel(const float* __restrict__ part_o,
-                                                            const float* __restrict__ part_ml,
-                                                            const int* __restrict__ seq_lens, int n_q,
-                                                            int max_splits, int split_tokens,
-                                                            bf16_t* __restrict__ out) {
-  const int bq = blockIdx.x;  // b * n_q + qh
+__global__ __launch_bounds__(64 * COMBINE_WAVES) void decode_combine_kernel(
+    const float* __restrict__ part_o, const float* __restrict__ part_ml, const int* __restrict__ seq_lens, int n_q,
+    int max_splits, int split_tokens, int n_bq, bf16_t* __restrict__ out) {
+  constexpr int PER = HD / 64;  // dims per lane
+  const int lane = threadIdx.x & 63;
+  const int bq = blockIdx.x * COMBINE_WAVES + (threadIdx.x >> 6);
+  if (bq >= n_bq) return;  // wave-uniform
   const int b = bq / n_q;
-  const int d = threadIdx.x;
-  const int ns = (seq_lens[b] + split_tokens - 1) / split_tokens;
-  const float* ml = part_ml + static_cast<size_t>(bq) * max_splits * 2;
-  float mm = -INFINITY;
-  for (int s = 0; s < ns; ++s) mm = fmaxf(mm, ml[2 * s]);
-  float ll = 0.f, oo = 0.f;
-  for (int s = 0; s < ns; ++s) {
-    const float f = ml[2 * s] == -INFINITY ? 0.f : exp2f(ml[2 * s] - mm);
-    ll += ml[2 * s + 1] * f;
-    oo += part_o[(static_cast<size_t>(bq) * max_splits + s) * HD + d] * f;
+  const int ns = (seq_lens[b] + split_tokens - 1) / split_tokens;  // <= max_splits <= 64 (host check)
+  const float2 mlv = lane < ns ? reinterpret_cast<const float2*>(part_ml)[static_cast<size_t>(bq) * max_splits + lane]
+                               : float2{-INFINITY, 0.f};
+  float mm = mlv.x;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mm = fmaxf(mm, __shfl_xor(mm, o, 64));
+  const float f = mlv.x == -INFINITY ? 0.f : exp2f(mlv.x - mm);
+  float ll = mlv.y * f;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) ll += __shfl_xor(ll, o, 64);
+  const float* po = part_o + static_cast<size_t>(bq) * max_splits * HD + lane * PER;
+  float acc[PER];
+#pragma unroll
+  for (int e = 0; e < PER; ++e) acc[e] = 0.f;
+  int s = 0;
+  for (; s + 4 <= ns; s += 4) {  // four splits' loads in flight before their FMAs
+    float v[4][PER];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < PER; ++e) v[j][e] = po[(s + j) * HD + e];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float fj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, f), s + j));
+#pragma unroll
+      for (int e = 0; e < PER; ++e) acc[e] += fj * v[j][e];
+    }
   }
-  out[static_cast<size_t>(bq) * HD + d] = f2bf(ll > 0.f ? oo / ll : 0.f);
+  for (; s < ns; ++s) {
+    const float fj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, f), s));
+#pragma unroll
+    for (int e = 0; e < PER; ++e) acc[e] += fj * po[s * HD + e];
+  }
+  const float inv = ll > 0.f ? 1.f / ll : 0.f;
+#pragma unroll
+  for (int e = 0; e < PER; ++e) out[static_cast<size_t>(bq) * HD + lane * PER + e] = f2bf(acc[e] * inv);
 }
 
 template <int HD, bool KT = false, bool F8 = false, int CPW = 1>
@@ -494,8 +526,10 @@ void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
   const int grid = static_cast<int>(std::min<long>(static_cast<long>(B) * g.n_kv * max_splits, resident));
   hipLaunchKernelGGL((decode_attn_kernel<HD, KT, F8, CPW>), dim3(grid), dim3(256), 0, stream, q, g, tables, max_blocks,
                      seq_lens, B, n_q, sl, part_o, part_ml, max_splits);
-  hipLaunchKernelGGL(decode_combine_kernel<HD>, dim3(B * n_q), dim3(HD), 0, stream, part_o, part_ml, seq_lens,
-                     n_q, max_splits, DEC_SPLIT, out);
+  const int n_bq = B * n_q;
+  hipLaunchKernelGGL(decode_combine_kernel<HD>, dim3((n_bq + COMBINE_WAVES - 1) / COMBINE_WAVES),
+                     dim3(64 * COMBINE_WAVES), 0, stream, part_o, part_ml, seq_lens, n_q, max_splits, DEC_SPLIT, n_bq,
+                     out);
 }
 
 // ----------------------------------------------------------------- prefill
@@ -848,6 +882,7 @@ BCG_API int bcg_paged_attention_decode(const void* q, const void* k_cache, const
                                        void* out, int kv_fp8, hipStream_t stream) {
   if (block_size != BS || n_q % n_kv || n_q / n_kv > 16 || B <= 0 || B > DEC_MAX_B) return -2;
   if (split_tokens != DEC_WAVES * CHUNK * DEC_CPW || max_splits * split_tokens < max_blocks * BS) return -3;
+  if (max_splits > 64) return -3;  // decode_combine_kernel: one lane per split
   KVGeom g{static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), layer, num_blocks, n_kv};
   const bf16_t* qb = static_cast<const bf16_t*>(q);
   bf16_t* ob = static_cast<bf16_t*>(out);
@@ -877,7 +912,8 @@ BCG_API int bcg_paged_attention_decode_exp(const void* q, const void* k_cache, c
                                            const int* seq_lens, int B, int n_q, int hd, float scale,
                                            float* workspace, int max_splits, int split_tokens, void* out,
                                            int variant, hipStream_t stream) {
-  if (hd != 128 || n_q / n_kv > 16 || split_tokens != DEC_WAVES * CHUNK || B > DEC_MAX_B) return -2;
+  if (hd != 128 || n_q / n_kv > 16 || split_tokens != DEC_WAVES * CHUNK || B > DEC_MAX_B || max_splits > 64)
+    return -2;
   KVGeom g{static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), layer, num_blocks, n_kv};
   const float sl = scale * LOG2E;
   if (variant == 2)  // two chunks per wave, both loaded up front (256-token items)

@@ -30,6 +30,15 @@
 //                 the kernel writes h[M, I] = silu(gate) * up directly (K-ACT fused)
 //   EPI_RESIDUAL  C = residual + acc (o_proj / down_proj: the residual stream
 //                 update of the following add+RMSNorm, fused)
+//
+// fp8 variant (F8 = true; the fp8-projection path of BASELINE config 5):
+//   C[m, n] = xs[m] * ws[n] * sum_k Xq[m, k] Wq[n, k]   (+ bias, + residual)
+// with OCP e4m3fn operands, a row-wise activation scale and a per-output-channel weight
+// scale (vLLM's dynamic per-token fp8 scheme).  The same 128-B LDS rows then hold 128 K
+// elements; each lane's two 16-B fragments of a tile (chunks fq and 4 + fq) form the
+// 32-byte operand of ONE block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (unit E8M0
+// scales): 2x the bf16 MFMA rate and half the bytes per K.  A and B use the same
+// lane -> k assignment, so the permuted k order inside the instruction cancels.
 #include "common.h"
 
 namespace {
@@ -48,8 +57,8 @@ __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); 
 // (row r at byte r*128, swizzled chunks).  Every wave issues rows/32 glds of 8 rows each.
 // `src_row(r)` maps a tile row to its global row.
 template <int ROWS, int NW, typename RowFn>
-__device__ __forceinline__ void stage_tile(unsigned char* lds, const bf16_t* __restrict__ g, int K, int k0,
-                                           RowFn src_row) {
+__device__ __forceinline__ void stage_tile(unsigned char* lds, const unsigned char* __restrict__ g, int row_bytes,
+                                           int k0_bytes, RowFn src_row) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr int PER_WAVE = ROWS / (8 * NW);  // 8 rows per glds, NW waves
   static_assert(PER_WAVE >= 1 && ROWS % (8 * NW) == 0, "tile rows per wave");
@@ -58,7 +67,7 @@ __device__ __forceinline__ void stage_tile(unsigned char* lds, const bf16_t* __r
     const int r = (wave * PER_WAVE + i) * 8 + (lane >> 3);
     const int phys = lane & 7;
     const int c = phys ^ ((r >> 1) & 7);  // logical chunk stored at this slot
-    const bf16_t* src = g + static_cast<size_t>(src_row(r)) * K + k0 + c * 8;
+    const unsigned char* src = g + static_cast<size_t>(src_row(r)) * row_bytes + k0_bytes + c * 16;
     __builtin_amdgcn_global_load_lds(src, lds + (wave * PER_WAVE + i) * 1024, 16, 0, 0);
   }
 }
@@ -88,12 +97,19 @@ __device__ __forceinline__ void block_sync_lds() {
   __builtin_amdgcn_s_barrier();
 }
 
-template <int BM, int BN, int WM, int WN, int S, int EPI>
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+template <int BM, int BN, int WM, int WN, int S, int EPI, bool F8 = false>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt_kernel(
-    const bf16_t* __restrict__ X, const bf16_t* __restrict__ W, const bf16_t* __restrict__ bias,
+    const void* __restrict__ Xv, const void* __restrict__ Wv, const bf16_t* __restrict__ bias,
     const bf16_t* __restrict__ residual, bf16_t* __restrict__ C, float* __restrict__ ws,
     int* __restrict__ counters, int M, int N, int K, int ldc, int inter, int m_tiles, int n_tiles,
-    int split_k) {
+    int split_k, const float* __restrict__ x_scale, const float* __restrict__ w_scale) {
+  const unsigned char* X = static_cast<const unsigned char*>(Xv);
+  const unsigned char* W = static_cast<const unsigned char*>(Wv);
+  constexpr int ESZ = F8 ? 1 : 2;      // bytes per element
+  constexpr int BKE = 128 / ESZ;       // K elements per tile (one 128-B LDS row)
   constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
   constexpr int MT = WTM / 16, NT = WTN / 16;
   constexpr int NW = WM * WN;
@@ -101,7 +117,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt_kernel(
   static_assert(EPI != EPI_SILU_MUL || NT % 2 == 0, "gate/up pairs per wave");
   static_assert(S >= 2, "at least double buffering");
   static_assert(MT + NT <= 15, "lgkmcnt counts at most 15 LDS reads");
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  static_assert(!F8 || EPI != EPI_SILU_MUL, "fp8: store / residual epilogues");
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
   constexpr int L = BM / (8 * NW) + BN / (8 * NW);  // glds per tile per wave
   // ONE shared array for everything (a second __shared__ object can make hipcc drain
   // vmcnt before every ds_read: cdna_hip_programming.md "Projection GEMM" item 4a)
@@ -117,7 +134,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt_kernel(
   const int tile = r_id / split_k;
   const int m_tile = tile % m_tiles, n_tile = tile / m_tiles;
   const int m0 = m_tile * BM, n0 = n_tile * BN;
-  const int nk_all = K / BK;
+  const int nk_all = K / BKE;
   const int kt0 = split * nk_all / split_k, kt1 = (split + 1) * nk_all / split_k;
   const int nk = kt1 - kt0;
 
@@ -137,9 +154,9 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt_kernel(
   };
   auto issue = [&](int t) {  // tile t (relative) -> stage t % S
     unsigned char* st = smem + (t % S) * STAGE;
-    const int k0 = (kt0 + t) * BK;
-    stage_tile<BM, NW>(st, X, K, k0, x_row);
-    stage_tile<BN, NW>(st + A_BYTES, W, K, k0, w_row);
+    const int k0b = (kt0 + t) * 128;
+    stage_tile<BM, NW>(st, X, K * ESZ, k0b, x_row);
+    stage_tile<BN, NW>(st + A_BYTES, W, K * ESZ, k0b, w_row);
   };
 
   f32x4 acc[NT][MT];
@@ -163,6 +180,24 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt_kernel(
       const int r = wn * WTN + i * 16 + fr;
       wb[i] = *reinterpret_cast<const bf16x8s*>(Bs + r * 128 + swz(r, chunk) * 16);
     }
+  };
+  // fp8: the two k-steps' fragments of a tile are one 32-byte operand (K = 128)
+  auto mfmas8 = [&](const bf16x8s (&xa)[MT], const bf16x8s (&wb)[NT], const bf16x8s (&xb)[MT],
+                    const bf16x8s (&wc)[NT]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      const i32x4 w0 = __builtin_bit_cast(i32x4, wb[i]), w1 = __builtin_bit_cast(i32x4, wc[i]);
+      const i32x8 wop = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        const i32x4 x0 = __builtin_bit_cast(i32x4, xa[j]), x1 = __builtin_bit_cast(i32x4, xb[j]);
+        const i32x8 xop = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+        // formats 0/0 = e4m3 x e4m3; E8M0 scale 127 = 1.0 for both operands
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wop, xop, acc[i][j], 0, 0, 0, 127, 0, 127);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
   };
   auto mfmas = [&](const bf16x8s (&xa)[MT], const bf16x8s (&wb)[NT]) {
     __builtin_amdgcn_s_setprio(1);
@@ -189,6 +224,17 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt_kernel(
   read_frags(0, 0, xa0, wb0);
   for (int kt = 0; kt < nk; ++kt) {
     read_frags(kt, 1, xa1, wb1);
+    if constexpr (F8) {  // one K = 128 MFMA per block pair over both k-steps' fragments
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      mfmas8(xa0, wb0, xa1, wb1);
+      if (kt + 1 < nk) {
+        wait_tiles<L, S - 2>(min(nk, kt + S) - kt - 2);
+        block_sync_lds();
+        if (kt + S < nk) issue(kt + S);
+        read_frags(kt + 1, 0, xa0, wb0);
+      }
+      continue;
+    }
     asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(MT + NT) : "memory");  // k-step 0 landed
     mfmas(xa0, wb0);
     if (kt + 1 < nk) {
@@ -268,6 +314,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_nt_kernel(
       for (int i = 0; i < NT; ++i) {
         const int n = n0 + wn * WTN + i * 16 + 4 * fq;
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if constexpr (F8) {  // dequantise: row scale x column scales
+          const float xs = x_scale[m];
+          const f32x4 wsc = *reinterpret_cast<const f32x4*>(w_scale + n);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] *= xs * wsc[e];
+        }
         if (bias != nullptr) {
           const u16x4 b = *reinterpret_cast<const u16x4*>(bias + n);
 #pragma unroll
@@ -296,32 +348,34 @@ constexpr TileCfg CFGS[] = {{128, 128, 4}, {64, 128, 5}, {128, 64, 5},  {256, 12
                             {64, 64, 6},   {32, 128, 6}, {256, 128, 3}, {128, 256, 3}, {128, 128, 4}};
 constexpr int N_CFG = sizeof(CFGS) / sizeof(CFGS[0]);
 
-template <int BM, int BN, int WM, int WN, int S, int EPI>
+template <int BM, int BN, int WM, int WN, int S, int EPI, bool F8 = false>
 int launch(const void* x, const void* w, const void* bias, const void* res, void* c, float* ws, int* cnt, int M,
-           int N, int K, int inter, int split_k, hipStream_t stream) {
+           int N, int K, int inter, int split_k, hipStream_t stream, const float* xs = nullptr,
+           const float* wsc = nullptr) {
   const int m_tiles = (M + BM - 1) / BM, n_tiles = N / BN;
   const int ldc = EPI == EPI_SILU_MUL ? inter : N;
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, S, EPI>), dim3(m_tiles * n_tiles * split_k),
-                     dim3(64 * WM * WN), 0, stream, static_cast<const bf16_t*>(x), static_cast<const bf16_t*>(w),
-                     static_cast<const bf16_t*>(bias), static_cast<const bf16_t*>(res), static_cast<bf16_t*>(c), ws,
-                     cnt, M, N, K, ldc, inter, m_tiles, n_tiles, split_k);
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, S, EPI, F8>), dim3(m_tiles * n_tiles * split_k),
+                     dim3(64 * WM * WN), 0, stream, x, w, static_cast<const bf16_t*>(bias),
+                     static_cast<const bf16_t*>(res), static_cast<bf16_t*>(c), ws, cnt, M, N, K, ldc, inter, m_tiles,
+                     n_tiles, split_k, xs, wsc);
   return BCG_CHECK_LAUNCH();
 }
 
-template <int EPI>
+template <int EPI, bool F8 = false>
 int dispatch(int cfg, const void* x, const void* w, const void* bias, const void* res, void* c, float* ws, int* cnt,
-             int M, int N, int K, int inter, int sk, hipStream_t s) {
+             int M, int N, int K, int inter, int sk, hipStream_t s, const float* xs = nullptr,
+             const float* wsc = nullptr) {
   switch (cfg) {
-    case 0: return launch<128, 128, 2, 2, 4, EPI>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s);
-    case 1: return launch<64, 128, 1, 4, 5, EPI>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s);
-    case 2: return launch<128, 64, 2, 2, 5, EPI>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s);
-    case 3: return launch<256, 128, 4, 1, 3, EPI>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s);
-    case 4: return launch<64, 256, 1, 4, 4, EPI>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s);
-    case 5: return launch<64, 64, 2, 2, 6, EPI>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s);
-    case 6: return launch<32, 128, 1, 4, 6, EPI>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s);
-    case 7: return launch<256, 128, 4, 2, 3, EPI>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s);
-    case 8: return launch<128, 256, 2, 4, 3, EPI>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s);
-    case 9: return launch<128, 128, 2, 4, 4, EPI>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s);
+    case 0: return launch<128, 128, 2, 2, 4, EPI, F8>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s, xs, wsc);
+    case 1: return launch<64, 128, 1, 4, 5, EPI, F8>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s, xs, wsc);
+    case 2: return launch<128, 64, 2, 2, 5, EPI, F8>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s, xs, wsc);
+    case 3: return launch<256, 128, 4, 1, 3, EPI, F8>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s, xs, wsc);
+    case 4: return launch<64, 256, 1, 4, 4, EPI, F8>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s, xs, wsc);
+    case 5: return launch<64, 64, 2, 2, 6, EPI, F8>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s, xs, wsc);
+    case 6: return launch<32, 128, 1, 4, 6, EPI, F8>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s, xs, wsc);
+    case 7: return launch<256, 128, 4, 2, 3, EPI, F8>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s, xs, wsc);
+    case 8: return launch<128, 256, 2, 4, 3, EPI, F8>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s, xs, wsc);
+    case 9: return launch<128, 128, 2, 4, 4, EPI, F8>(x, w, bias, res, c, ws, cnt, M, N, K, inter, sk, s, xs, wsc);
     default: return -2;
   }
 }
@@ -370,6 +424,30 @@ BCG_API int bcg_gemm_nt(int cfg, int epi, const void* x, const void* w, const vo
     case EPI_RESIDUAL:
       if (!residual) return -2;
       return dispatch<EPI_RESIDUAL>(cfg, x, w, bias, residual, c, wsf, cnt, M, N, K, inter, split_k, stream);
+    default: return -2;
+  }
+}
+
+// fp8 (e4m3fn) projection GEMM: C = x_scale[m] * w_scale[n] * (Xq . Wq^T) (+ bias) (+ residual).
+// epi: 0 = store, 2 = residual + result.  Requirements: K % 128 == 0, K/128 >= split_k,
+// N % BN == 0 (cfg's tile), x_scale [M] / w_scale [N] fp32, pointers 16-B aligned; split-K
+// workspace / counters as bcg_gemm_nt.
+BCG_API int bcg_gemm_nt_fp8(int cfg, int epi, const void* xq, const void* wq, const float* x_scale,
+                            const float* w_scale, const void* bias, const void* residual, void* c, void* ws,
+                            void* counters, int M, int N, int K, int split_k, hipStream_t stream) {
+  if (M <= 0 || K % 128 || K <= 0 || split_k < 1 || K / 128 < split_k || !x_scale || !w_scale) return -2;
+  if (split_k > 1 && (!ws || !counters)) return -2;
+  if (cfg < 0 || cfg >= N_CFG || N % CFGS[cfg].bn) return -2;
+  float* wsf = static_cast<float*>(ws);
+  int* cnt = static_cast<int*>(counters);
+  switch (epi) {
+    case EPI_STORE:
+      return dispatch<EPI_STORE, true>(cfg, xq, wq, bias, residual, c, wsf, cnt, M, N, K, 0, split_k, stream,
+                                       x_scale, w_scale);
+    case EPI_RESIDUAL:
+      if (!residual) return -2;
+      return dispatch<EPI_RESIDUAL, true>(cfg, xq, wq, bias, residual, c, wsf, cnt, M, N, K, 0, split_k, stream,
+                                          x_scale, w_scale);
     default: return -2;
   }
 }

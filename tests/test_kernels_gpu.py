@@ -122,6 +122,23 @@ def test_paged_attention_decode_shared_workspace_buckets(hip):
             _close(out, ref, atol=2e-2)
 
 
+def test_paged_attention_decode_large_batch(hip):
+    """Beyond 1024 rows (the item prefix sum spans 8 entries per thread) with short and
+    long contexts mixed: every row matches the reference."""
+    gen = torch.Generator().manual_seed(9)
+    n_q, n_kv, hd, NB, max_blocks = 40, 8, 128, 1024, 64
+    B = 1500
+    k, v = _caches(1, NB, n_kv, hd)
+    lens = torch.randint(1, 1000, (B,), generator=gen).tolist()
+    tables = torch.randint(1, NB, (B, max_blocks), generator=gen, dtype=torch.int32).cuda()
+    seq = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    q = torch.randn(B, n_q, hd, device="cuda", dtype=torch.bfloat16)
+    ref = R.paged_attention(q, k, v, 0, tables, torch.arange(B + 1, dtype=torch.int32, device="cuda"), seq,
+                            hd ** -0.5)
+    out = hip.paged_attention_decode(q, k, v, 0, tables, seq, hd ** -0.5)
+    _close(out, ref, atol=2e-2)
+
+
 def _prefill_tiles(q_start, seq_lens):
     tiles = []
     for i in range(len(q_start) - 1):
