@@ -38,6 +38,11 @@ constexpr int CHUNK = 32;
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float RESCALE_LOG2 = 8.f;  // lazy online-softmax rescale threshold (log2 units)
 
+// 2^x as the bare v_exp_f32.  exp2f() wraps it in a denormal range reduction (v_cmp +
+// v_cndmask + v_ldexp around every exponential: ~3 extra VALU per score); softmax
+// arguments are <= 0 here and a result below 2^-126 may flush to 0.
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 struct KVGeom {
   const bf16_t* k;   // [L, NB, n_kv, BS, HD]
   const bf16_t* v;   // [L, NB, n_kv, HD, BS]
@@ -185,7 +190,7 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16
   if constexpr (LAZY) {
     if (__builtin_amdgcn_ballot_w64(mx > m + RESCALE_LOG2) != 0) {  // wave-uniform
       const float m_new = fmaxf(m, mx);
-      const float alpha = m == -INFINITY ? 0.f : exp2f(m - m_new);
+      const float alpha = m == -INFINITY ? 0.f : fast_exp2(m - m_new);
       l *= alpha;
 #pragma unroll
       for (int dt = 0; dt < HD / 16; ++dt) o[dt] *= alpha;
@@ -197,7 +202,7 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16
   float alpha = 1.f;
   if constexpr (!LAZY) {
     const float m_new = fmaxf(m, mx);
-    alpha = m == -INFINITY ? 0.f : exp2f(m - (m_new == -INFINITY ? 0.f : m_new));
+    alpha = m == -INFINITY ? 0.f : fast_exp2(m - (m_new == -INFINITY ? 0.f : m_new));
     l *= alpha;
     m = m_new;
   }
@@ -205,7 +210,7 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16
   float ps = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    p[j] = exp2f(p[j] - m_use);
+    p[j] = fast_exp2(p[j] - m_use);
     ps += p[j];
   }
   ps = rows_sum(ps);
@@ -243,15 +248,18 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16
 // All NT query sub-tiles of a wave on one chunk that every row of every sub-tile sees in
 // full (no mask), as ONE straight-line block: the S^T MFMAs of every sub-tile first, then
 // each sub-tile's softmax (its VALU runs while the later sub-tiles' MFMAs are still in the
-// pipe), then every P.V MFMA.  Lazy rescale with ONE wave-uniform branch for all
-// sub-tiles (taken only when some column's running max moves by > 2^RESCALE_LOG2): the
-// per-sub-tile branches of compute_chunk split the chunk into basic blocks the compiler
-// cannot interleave.
-template <int HD, int NT, bool F8, typename ReloadK, typename ReloadV>
-__device__ __forceinline__ void compute_chunk_full(Chunk<HD, F8>& c, const bf16x8 (&bq)[NT][HD / 32],
-                                                   float scale_log2, float (&m)[NT], float (&l)[NT],
-                                                   f32x4 (&o)[NT][HD / 16], ReloadK reload_k, ReloadV reload_v) {
-  f32x4 s[NT][2];
+// pipe), then every P.V MFMA.  Split in two so the caller's loop can leave for the (rare,
+// lazy: only when some column's running max moves by > 2^RESCALE_LOG2) rescale of O:
+//   full_scores  S^T MFMAs, the next chunk's K reloaded in place, per-column chunk max;
+//                returns whether any column needs a rescale (wave-uniform);
+//   full_pv      P = exp2(S - m), l += rowsum(P), O^T += V^T P^T, next chunk's V reloaded.
+// With the rescale (VALU on the O accumulators) inside the loop body, hipcc copied all
+// 128 O accumulators AGPR -> VGPR at the top of EVERY chunk, taken or not (128
+// v_accvgpr_read per 64 MFMAs at NT = 4); outside it, O stays in AGPRs.
+template <int HD, int NT, bool F8, typename ReloadK>
+__device__ __forceinline__ bool full_scores(Chunk<HD, F8>& c, const bf16x8 (&bq)[NT][HD / 32], float scale_log2,
+                                            const float (&m)[NT], f32x4 (&s)[NT][2], float (&mx)[NT],
+                                            ReloadK reload_k) {
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -262,7 +270,6 @@ __device__ __forceinline__ void compute_chunk_full(Chunk<HD, F8>& c, const bf16x
         s[nt][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(to_bf16x8(c.k[u][kk]), bq[nt][kk], s[nt][u], 0, 0, 0);
     }
   reload_k(c);  // next chunk's K into the registers the S^T MFMAs just read
-  float mx[NT];
   bool grow = false;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
@@ -271,24 +278,20 @@ __device__ __forceinline__ void compute_chunk_full(Chunk<HD, F8>& c, const bf16x
     mx[nt] = rows_max(v * scale_log2);
     grow |= mx[nt] > m[nt] + RESCALE_LOG2;
   }
-  if (__builtin_amdgcn_ballot_w64(grow) != 0) {  // wave-uniform, rare after the first chunks
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const float m_new = fmaxf(m[nt], mx[nt]);
-      const float alpha = m[nt] == -INFINITY ? 0.f : exp2f(m[nt] - m_new);
-      l[nt] *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt) o[nt][dt] *= alpha;
-      m[nt] = m_new;
-    }
-  }
+  return __builtin_amdgcn_ballot_w64(grow) != 0;
+}
+
+template <int HD, int NT, bool F8, typename ReloadV>
+__device__ __forceinline__ void full_pv(Chunk<HD, F8>& c, const f32x4 (&s)[NT][2], float scale_log2,
+                                        const float (&m)[NT], float (&l)[NT], f32x4 (&o)[NT][HD / 16],
+                                        ReloadV reload_v) {
   bf16x8 bp[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     float ps = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float pj = exp2f(s[nt][j >> 2][j & 3] * scale_log2 - m[nt]);
+      const float pj = fast_exp2(s[nt][j >> 2][j & 3] * scale_log2 - m[nt]);
       ps += pj;
       bp[nt][j] = static_cast<__bf16>(pj);
     }
@@ -300,6 +303,20 @@ __device__ __forceinline__ void compute_chunk_full(Chunk<HD, F8>& c, const bf16x
     for (int dt = 0; dt < HD / 16; ++dt)
       o[nt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(to_bf16x8(c.v[dt]), bp[nt], o[nt][dt], 0, 0, 0);
   reload_v(c);
+}
+
+template <int HD, int NT>
+__device__ __forceinline__ void full_rescale(const float (&mx)[NT], float (&m)[NT], float (&l)[NT],
+                                             f32x4 (&o)[NT][HD / 16]) {
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const float m_new = fmaxf(m[nt], mx[nt]);
+    const float alpha = m[nt] == -INFINITY ? 0.f : fast_exp2(m[nt] - m_new);
+    l[nt] *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) o[nt][dt] *= alpha;
+    m[nt] = m_new;
+  }
 }
 
 template <int HD>
@@ -545,7 +562,7 @@ void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
 #define PREFILL_LAZY false  // measured: see PERF.md (lazy spills at NT = 4)
 #endif
 #ifndef PREFILL_FULL_BLOCK
-#define PREFILL_FULL_BLOCK 1  // fully visible chunks through compute_chunk_full (lazy rescale, in-place reload)
+#define PREFILL_FULL_BLOCK 1  // fully visible chunks through full_scores / full_pv (lazy rescale outside the inner loop, in-place reload)
 #endif
 #ifndef PREFILL_WPE
 #define PREFILL_WPE 0
@@ -617,17 +634,28 @@ __global__ __launch_bounds__(256) PREFILL_ATTR void prefill_attn_kernel(
   // the next chunk reloaded in place (K after the S^T MFMAs, V after the P.V MFMAs): no
   // second register set for the prefetch
   int c = 0;
-  for (; (c + 1) * CHUNK <= sub_first[0] && c < nchunk; ++c) {
-    const int cn = min(c + 1, nchunk - 1);
-    const int b0 = block_at(2 * cn), b1 = block_at(min(2 * cn + 1, nblk - 1));
-#ifdef PREFILL_ABL_NORELOAD  // timing-only ablation: every chunk reuses chunk 0's K/V
-    (void)b0, (void)b1;
-    compute_chunk_full<HD, NT, F8>(cur, bq, scale_log2, m, l, o, [](Chunk<HD, F8>&) {}, [](Chunk<HD, F8>&) {});
-#else
-    compute_chunk_full<HD, NT, F8>(
-        cur, bq, scale_log2, m, l, o, [&](Chunk<HD, F8>& x) { load_chunk_k<HD, F8>(x, g, b0, b1, kvh, lane); },
-        [&](Chunk<HD, F8>& x) { load_chunk_v<HD, F8>(x, g, b0, b1, kvh, lane); });
-#endif
+  const int n_full = min(sub_first[0] / CHUNK, nchunk);  // chunks every row of the wave sees in full
+  while (c < n_full) {
+    f32x4 s[NT][2];
+    float mx[NT];
+    bool grow = false;
+    int b0 = 0, b1 = 0;
+    // inner loop: no VALU on O (it stays in the MFMA accumulators); leaves with S live
+    // when a column's max moved enough to need the lazy rescale
+    for (; c < n_full; ++c) {
+      const int cn = min(c + 1, nchunk - 1);
+      b0 = block_at(2 * cn), b1 = block_at(min(2 * cn + 1, nblk - 1));
+      grow = full_scores<HD, NT, F8>(cur, bq, scale_log2, m, s, mx,
+                                     [&](Chunk<HD, F8>& x) { load_chunk_k<HD, F8>(x, g, b0, b1, kvh, lane); });
+      if (grow) break;  // wave-uniform
+      full_pv<HD, NT, F8>(cur, s, scale_log2, m, l, o,
+                          [&](Chunk<HD, F8>& x) { load_chunk_v<HD, F8>(x, g, b0, b1, kvh, lane); });
+    }
+    if (!grow) break;
+    full_rescale<HD, NT>(mx, m, l, o);
+    full_pv<HD, NT, F8>(cur, s, scale_log2, m, l, o,
+                        [&](Chunk<HD, F8>& x) { load_chunk_v<HD, F8>(x, g, b0, b1, kvh, lane); });
+    ++c;
   }
   Chunk<HD, F8> nxt;
   for (; c < nchunk; ++c) {
