@@ -19,8 +19,12 @@ def main(root):
                 acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
     for name, counters in sorted(acc.items()):
         print(name)
+        mean = {}
         for c, vals in sorted(counters.items()):
-            print(f"    {c:36s} n={len(vals):5d} mean={sum(vals) / len(vals):16.1f}")
+            mean[c] = sum(vals) / len(vals)
+            print(f"    {c:36s} n={len(vals):5d} mean={mean[c]:16.1f}")
+        if mean.get("SQ_INSTS_MFMA"):
+            print(f"    VALU per MFMA instruction           {mean.get('SQ_INSTS_VALU', 0.0) / mean['SQ_INSTS_MFMA']:16.2f}")
 
 
 if __name__ == "__main__":
