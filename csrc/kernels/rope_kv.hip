@@ -85,6 +85,96 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kv_kernel(
   }
 }
 
+// Vectorised form (hd = 64 or 128): a lane owns 4 consecutive dims of each half of one head
+// (8-B loads and stores instead of 2-B ones), LPH = hd/8 lanes per head, 64/LPH heads per wave,
+// the head RMS reduced over the LPH lanes with xor shuffles.  Token metadata (slot,
+// position, cos/sin row) is loaded once per lane group.  The one-wave-per-head form above
+// moved 2 bytes per lane per access and was latency-bound at decode sizes (34 us per layer
+// at 616 rows, ~10x its byte time).
+template <typename CacheT, int HD>
+__global__ __launch_bounds__(256) void qk_norm_rope_kv_vec_kernel(
+    const bf16_t* __restrict__ qkv, const int* __restrict__ positions, const int* __restrict__ slots,
+    bf16_t* __restrict__ q_out, const bf16_t* __restrict__ q_norm, const bf16_t* __restrict__ k_norm,
+    const float* __restrict__ cos_sin, CacheT* __restrict__ k_cache, CacheT* __restrict__ v_cache,
+    int layer, int T, int n_q, int n_kv, int num_blocks, int block_size, float eps) {
+  constexpr int HALF = HD / 2, LPH = HALF / 4, HPW = 64 / LPH;  // lanes per head, heads per wave
+  const int lane = threadIdx.x & 63, li = lane % LPH;
+  const int slot_head = (blockIdx.y * 4 + (threadIdx.x >> 6)) * HPW + lane / LPH;
+  const int t = blockIdx.x;
+  const int n_heads = n_q + 2 * n_kv;
+  if (t >= T) return;
+  const bool valid = slot_head < n_heads;  // idle lanes still take part in the shuffles
+  const int d0 = 4 * li;
+  const bf16_t* src = qkv + (static_cast<size_t>(t) * n_heads + (valid ? slot_head : 0)) * HD;
+  u16x4 a = *reinterpret_cast<const u16x4*>(src + d0), bv = *reinterpret_cast<const u16x4*>(src + HALF + d0);
+  float x1[4], x2[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) x1[e] = bf2f(a[e]), x2[e] = bf2f(bv[e]);
+  const int slot = slots[t];
+  const int blk = slot / block_size, off = slot % block_size;
+
+  if (slot_head >= n_q + n_kv) {  // value head (or idle): transposed store, no transform
+    if (!valid) return;
+    const int h = slot_head - n_q - n_kv;
+    CacheT* vb = v_cache + ((static_cast<size_t>(layer) * num_blocks + blk) * n_kv + h) * HD * block_size + off;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      vb[static_cast<size_t>(d0 + e) * block_size] = to_cache<CacheT>(x1[e]);
+      vb[static_cast<size_t>(HALF + d0 + e) * block_size] = to_cache<CacheT>(x2[e]);
+    }
+    return;
+  }
+  // (the branch above is uniform per lane group; the shuffles below stay within a group
+  //  of query/key heads, whose lanes all reach them)
+  const bool is_q = slot_head < n_q;
+  const bf16_t* nw = is_q ? q_norm : k_norm;
+  if (nw != nullptr) {
+    float ss = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ss += x1[e] * x1[e] + x2[e] * x2[e];
+#pragma unroll
+    for (int o = LPH / 2; o >= 1; o >>= 1) ss += __shfl_xor(ss, o, 64);
+    const float inv = rsqrtf(ss / HD + eps);
+    const u16x4 w1 = *reinterpret_cast<const u16x4*>(nw + d0), w2 = *reinterpret_cast<const u16x4*>(nw + HALF + d0);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x1[e] *= inv * bf2f(w1[e]), x2[e] *= inv * bf2f(w2[e]);
+  }
+  const float* cs = cos_sin + static_cast<size_t>(positions[t]) * HD;
+  const f32x4 c = *reinterpret_cast<const f32x4*>(cs + d0), sn = *reinterpret_cast<const f32x4*>(cs + HALF + d0);
+  float y1[4], y2[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) y1[e] = x1[e] * c[e] - x2[e] * sn[e], y2[e] = x2[e] * c[e] + x1[e] * sn[e];
+  if (is_q) {
+    bf16_t* dst = q_out + (static_cast<size_t>(t) * n_q + slot_head) * HD;
+    u16x4 o1, o2;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o1[e] = f2bf(y1[e]), o2[e] = f2bf(y2[e]);
+    *reinterpret_cast<u16x4*>(dst + d0) = o1;
+    *reinterpret_cast<u16x4*>(dst + HALF + d0) = o2;
+  } else {
+    const int h = slot_head - n_q;
+    CacheT* dst = k_cache + (((static_cast<size_t>(layer) * num_blocks + blk) * n_kv + h) * block_size + off) * HD;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      dst[d0 + e] = to_cache<CacheT>(y1[e]);
+      dst[HALF + d0 + e] = to_cache<CacheT>(y2[e]);
+    }
+  }
+}
+
+template <typename CacheT, int HD>
+void launch_vec(const void* qkv, const int* positions, const int* slots, void* q_out, const void* q_norm,
+                const void* k_norm, const float* cos_sin, void* k_cache, void* v_cache, int layer, int T, int n_q,
+                int n_kv, int num_blocks, int block_size, float eps, hipStream_t stream) {
+  constexpr int HPB = 4 * (64 / (HD / 8));  // heads per 256-thread block
+  const int n_heads = n_q + 2 * n_kv;
+  hipLaunchKernelGGL((qk_norm_rope_kv_vec_kernel<CacheT, HD>), dim3(T, (n_heads + HPB - 1) / HPB), dim3(256), 0,
+                     stream, static_cast<const bf16_t*>(qkv), positions, slots, static_cast<bf16_t*>(q_out),
+                     static_cast<const bf16_t*>(q_norm), static_cast<const bf16_t*>(k_norm), cos_sin,
+                     static_cast<CacheT*>(k_cache), static_cast<CacheT*>(v_cache), layer, T, n_q, n_kv, num_blocks,
+                     block_size, eps);
+}
+
 }  // namespace
 
 BCG_API int bcg_qk_norm_rope_kv_write(const void* qkv, const int* positions, const int* slots, void* q_out,
@@ -93,6 +183,24 @@ BCG_API int bcg_qk_norm_rope_kv_write(const void* qkv, const int* positions, con
                                       int hd, int num_blocks, int block_size, float eps, int kv_fp8,
                                       hipStream_t stream) {
   if (hd > 128 || (hd & 1) || T <= 0) return -2;
+  if (hd == 128 || hd == 64) {
+    if (kv_fp8) {
+      if (hd == 128)
+        launch_vec<uint8_t, 128>(qkv, positions, slots, q_out, q_norm, k_norm, cos_sin, k_cache, v_cache, layer, T,
+                                 n_q, n_kv, num_blocks, block_size, eps, stream);
+      else
+        launch_vec<uint8_t, 64>(qkv, positions, slots, q_out, q_norm, k_norm, cos_sin, k_cache, v_cache, layer, T,
+                                n_q, n_kv, num_blocks, block_size, eps, stream);
+    } else {
+      if (hd == 128)
+        launch_vec<bf16_t, 128>(qkv, positions, slots, q_out, q_norm, k_norm, cos_sin, k_cache, v_cache, layer, T,
+                                n_q, n_kv, num_blocks, block_size, eps, stream);
+      else
+        launch_vec<bf16_t, 64>(qkv, positions, slots, q_out, q_norm, k_norm, cos_sin, k_cache, v_cache, layer, T,
+                               n_q, n_kv, num_blocks, block_size, eps, stream);
+    }
+    return BCG_CHECK_LAUNCH();
+  }
   const int n_heads = n_q + 2 * n_kv;
   dim3 grid(T, (n_heads + HEADS_PER_BLOCK - 1) / HEADS_PER_BLOCK);
   if (kv_fp8)

@@ -85,6 +85,24 @@ def main():
             rec[f"v{variant}_TBps"] = round(gb / tv * 1e3, 2)
         out["attention"].append(rec)
         print(json.dumps(rec), flush=True)
+    # fused QK-norm + RoPE + paged KV write (decode rows and a prefill chunk)
+    from byzantine_consensus_llm_agents_amd.ops.reference import rope_cache
+    cs = rope_cache(8192, hd, 1e6, "cuda")
+    n_q, n_kv = cfg.num_heads, cfg.num_kv_heads
+    out["rope"] = []
+    for T in (616, 16384):
+        nbk = T // 16 + 2
+        kc = torch.zeros(1, nbk, n_kv, 16, hd, device="cuda", dtype=torch.bfloat16)
+        vc = torch.zeros(1, nbk, n_kv, hd, 16, device="cuda", dtype=torch.bfloat16)
+        qkv = torch.randn(T, (n_q + 2 * n_kv) * hd, device="cuda", dtype=torch.bfloat16)
+        pos = torch.randint(0, 4000, (T,), device="cuda", dtype=torch.int32)
+        slots = torch.randperm(nbk * 16, device="cuda")[:T].to(torch.int32)
+        wn = torch.ones(hd, device="cuda", dtype=torch.bfloat16)
+        t = timeit(lambda: hip.qk_norm_rope_kv_write(qkv, pos, slots, n_q, n_kv, hd, wn, wn, 1e-6, cs, kc, vc, 0))
+        gb = (qkv.numel() * 2 + T * n_q * hd * 2 + T * 2 * n_kv * hd * 2) / 1e9
+        rec = {"T": T, "rope_us": round(t, 1), "TBps": round(gb / t * 1e3, 2)}
+        out["rope"].append(rec)
+        print(json.dumps(rec), flush=True)
     # sampler
     V = cfg.vocab_size
     for B in (40, 160):
