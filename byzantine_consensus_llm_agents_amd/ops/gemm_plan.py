@@ -110,3 +110,37 @@ class GemmPlan:
             return None
         cfg = self.default_cfg(M)
         return (cfg, 1) if self.supported(cfg, M, N, K, epi) else None
+
+
+FP8_TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "engine", "tuned",
+                         "hand_gemm_fp8.json")
+FP8_RULE_MAX_M = 128  # unmeasured shapes: the hand fp8 kernel up to this M (it won every measured M <= 128)
+
+
+class Fp8Plan:
+    """Which fp8 projection GEMM runs: the hand block-scaled MFMA kernel (gemm.hip, F8) or
+    hipBLASLt's ``torch._scaled_mm``.  Measured shapes (``engine/tuned/hand_gemm_fp8.json``,
+    ``tools/bench_fp8_gemm.py``): the choice at the nearest measured M >= M, the library
+    beyond the largest measured M; unmeasured shapes: the hand kernel up to FP8_RULE_MAX_M."""
+
+    def __init__(self, tiles: Dict[int, Tuple[int, int]], table: Optional[str] = FP8_TABLE):
+        self.tiles = tiles
+        self.table: Dict[Tuple[int, int, int], Tuple[int, int]] = {}
+        if table and os.path.exists(table):
+            with open(table) as fh:
+                for key, ch in json.load(fh).get("choice", {}).items():
+                    self.table[tuple(map(int, key.split(",")))] = tuple(ch)
+
+    def choose(self, M: int, N: int, K: int) -> Optional[Tuple[int, int]]:
+        if os.environ.get("BCG_HAND_GEMM", "1") == "0" or K % 128 or M <= 0:
+            return None
+        above = [m for (m, n, k) in self.table if (n, k) == (N, K) and m >= M]
+        if above:
+            cfg, split = self.table[(min(above), N, K)]
+        elif any((n, k) == (N, K) for (_, n, k) in self.table) or M > FP8_RULE_MAX_M:
+            return None
+        else:
+            cfg, split = (6 if M <= 32 else 1 if M <= 64 else 0), 1
+        if cfg < 0 or cfg not in self.tiles or cfg == PP_CFG or N % self.tiles[cfg][1] or K // 128 < split:
+            return None
+        return (cfg, split)

@@ -395,34 +395,9 @@ def hip_ops() -> SimpleNamespace:
                                    M, N, K, split_k, _stream()), "gemm_nt_fp8")
         return out
 
-    fp8_table = {}
-    _fp8_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "engine", "tuned",
-                             "hand_gemm_fp8.json")
-    if os.path.exists(_fp8_path):
-        import json
-        with open(_fp8_path) as fh:
-            for key, ch in json.load(fh).get("choice", {}).items():
-                fp8_table[tuple(map(int, key.split(",")))] = tuple(ch)
-
-    def fp8_cfg(M, N, K):
-        """(tile, split-K) of the hand fp8 GEMM, or None for hipBLASLt (torch._scaled_mm).
-        Measured shapes (engine/tuned/hand_gemm_fp8.json, tools/bench_fp8_gemm.py): the
-        choice at the nearest measured M >= M; beyond the largest measured M the library.
-        Unmeasured shapes: the hand kernel up to M = 128 (where it won for every measured
-        projection), hipBLASLt above."""
-        mode = os.environ.get("BCG_HAND_GEMM", "1")
-        if mode == "0" or K % 128:
-            return None
-        above = [m for (m, n, k) in fp8_table if (n, k) == (N, K) and m >= M]
-        if above:
-            cfg, split = fp8_table[(min(above), N, K)]
-        elif any((n, k) == (N, K) for (_, n, k) in fp8_table) or M > 128:
-            return None
-        else:
-            cfg, split = (6 if M <= 32 else 1 if M <= 64 else 0), 1
-        if cfg < 0 or N % plan.tiles[cfg][1] or K // 128 < split:
-            return None
-        return (cfg, split)
+    from .gemm_plan import Fp8Plan
+    fp8_plan = Fp8Plan(plan.tiles)
+    fp8_cfg = fp8_plan.choose
 
     def linear_fp8(xq, xs, wq, ws, bias=None, out_dtype=torch.bfloat16):
         """fp8 projection with row-wise activation and per-channel weight scales: the hand

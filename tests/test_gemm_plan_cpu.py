@@ -44,3 +44,28 @@ def test_avoid_library_picks_fastest_hand_config(tmp_path, monkeypatch):
     assert p.choose(768, 34816, 5120, 1) == (10, 1)
     assert p.choose(16384, 5120, 17408, 2) == (PP_CFG, 1)  # unmeasured: the 256x256 kernel
     assert p.choose(5, 4096, 4096, 0) is not None
+
+
+def test_fp8_plan_table_rule_and_library(tmp_path, monkeypatch):
+    """fp8 projections: measured shapes follow the table (nearest M above, library beyond the
+    largest measured M or where it won), unmeasured shapes the hand kernel up to M = 128."""
+    from byzantine_consensus_llm_agents_amd.ops.gemm_plan import FP8_TABLE, TILES, Fp8Plan
+    monkeypatch.setenv("BCG_HAND_GEMM", "1")
+    path = tmp_path / "f8.json"
+    path.write_text(json.dumps({"choice": {"64,8192,6144": [5, 2], "256,8192,6144": [9, 2],
+                                           "320,8192,6144": [-1, 1]}}))
+    tiles = dict(enumerate(TILES))
+    p = Fp8Plan(tiles, str(path))
+    assert p.choose(40, 8192, 6144) == (5, 2)
+    assert p.choose(200, 8192, 6144) == (9, 2)
+    assert p.choose(300, 8192, 6144) is None       # library measured faster
+    assert p.choose(600, 8192, 6144) is None       # beyond the measured range
+    assert p.choose(100, 4096, 6144) == (0, 1)     # unmeasured shape: rule
+    assert p.choose(16, 4096, 6144) == (6, 1)
+    assert p.choose(200, 4096, 6144) is None
+    assert p.choose(64, 4096, 6100) is None        # K % 128
+    monkeypatch.setenv("BCG_HAND_GEMM", "0")
+    assert p.choose(40, 8192, 6144) is None
+    monkeypatch.setenv("BCG_HAND_GEMM", "1")
+    shipped = Fp8Plan(tiles, FP8_TABLE)            # the shipped Mistral-22B table loads and is usable
+    assert shipped.table and shipped.choose(160, 8192, 6144) is not None
