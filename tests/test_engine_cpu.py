@@ -165,3 +165,17 @@ def test_synthetic_tokenizer_is_pinned(monkeypatch):
     monkeypatch.delenv("BCG_ALLOW_UNPINNED_TOKENIZER", raising=False)
     with pytest.raises(RuntimeError, match="pinned"):
         T.synthetic_json("mistral")
+
+
+def test_decode_buckets_cover_every_batch_size():
+    """Every decode batch size up to the largest bucket maps to the smallest bucket >= it;
+    32-row steps up to 1024 rows (GEMM padding <= 31 rows), 64-row steps beyond."""
+    from byzantine_consensus_llm_agents_amd.engine.graphs import BUCKETS, MAX_ROWS, bucket_for
+    assert list(BUCKETS) == sorted(set(BUCKETS)) and MAX_ROWS == BUCKETS[-1] == 1536
+    for n in range(1, MAX_ROWS + 1):
+        b = bucket_for(n)
+        assert b >= n and all(x < n for x in BUCKETS if x < b)
+        if 160 < n <= 1024:
+            assert b - n < 32
+        elif n > 1024:
+            assert b - n < 64
