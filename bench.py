@@ -337,6 +337,7 @@ def main(argv=None):
             "config": {"model": model, "honest": args.honest, "byzantine": args.byzantine,
                        "global_batch": args.sims_per_gpu * (args.honest + args.byzantine) * (world // args.tp),
                        "sims_per_gpu": args.sims_per_gpu, "seq_len": C.VLLM_CONFIG["max_model_len"],
+                       "max_batch_seqs": C.ENGINE_CONFIG["max_batch_seqs"],
                        "max_tokens_decide": C.LLM_CONFIG["max_tokens_decide"],
                        "max_tokens_vote": C.LLM_CONFIG["max_tokens_vote"],
                        "step": f"{args.window_s:g} s window of the continuously-batched pool",

@@ -53,6 +53,9 @@ def test_bench_self_launches_two_ranks(tp, parallelism, replicas):
 def test_bench_single_rank_defaults_contract():
     out = _run(["--steps", "3", "--warmup", "1"])
     assert out["n_gpus"] == 1 and out["steps"] == 3 and out["config"]["parallelism"] == "dp1"
+    assert out["config"]["max_batch_seqs"] == 768 and out["config"]["sims_per_gpu"] == 2
+    out = _run(["--steps", "1", "--warmup", "1", "--max-batch-seqs", "1024"])
+    assert out["config"]["max_batch_seqs"] == 1024
     assert out["config"]["model"] == "Qwen/Qwen3-14B" and out["dtype"] == "bf16"
     assert out["config"]["honest"] == 4 and out["config"]["byzantine"] == 1
 
