@@ -26,6 +26,7 @@
 // head), causal over cached prefix + new tokens, varlen via a tile table.
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -839,6 +840,185 @@ __global__ __launch_bounds__(256) void prefill_attn_lds_kernel(
   }
 }
 
+// ---- prefill, K/V staged global -> LDS by DMA (glds), 3-chunk ring ------------------
+// The register-direct kernel above is fed L2 -> CU: every wave loads its own K/V (16 KB
+// per 32-token chunk for 64 MFMAs at NT = 4; NT = 2 with twice the bytes per MFMA is
+// slower, so the feed is the limit).  Here a workgroup = 4 waves x 16 query rows x GT
+// heads of ONE kv head, and each K/V byte crosses L2 -> CU once per workgroup: a chunk
+// (8 KB K + 8 KB V) is 16 global_load_lds of 1 KB (waves 0-1: K rows, waves 2-3: V dims),
+// no staging registers, issued two chunks ahead into a ring of three 16-KB slots.
+// Per chunk c:  vmcnt(chunks issued after c) -> s_barrier -> glds of chunk c + 2 into the
+// slot chunk c - 1 used -> ds_read fragments of chunk c -> MFMAs.  RAW: a slot is read
+// after its issuing threads' counted vmcnt and a barrier; WAR: it is refilled only after
+// the barrier every wave passes once its reads of the previous use have been consumed.
+// Same swizzled images as the register-staged kernel (rows of K: 16 x 16-B pieces,
+// piece j at j ^ k_swz(t); rows of V^T: 4 pieces, piece hh at hh ^ ((d >> 2) & 3)): glds
+// writes lane l's 16 B at slot l, so the swizzle is applied to each lane's SOURCE piece.
+#ifndef DMA_RING
+#define DMA_RING 3  // 16-KB chunk slots (LEAD = DMA_RING - 1 chunks loaded ahead; 5 measured the same)
+#endif
+#ifndef DMA_LAZY
+#define DMA_LAZY false  // eager rescale: the lazy branch per head spills at GT = 5
+#endif
+constexpr int DMA_CHUNK_BYTES = LDS_K_BYTES + LDS_V_BYTES;  // 16 KiB
+
+template <int GT>
+__global__ __launch_bounds__(256, 1) void prefill_attn_dma_kernel(
+    const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
+    const int* __restrict__ q_start, const int* __restrict__ seq_lens, const int* __restrict__ tiles,
+    int n_q, float scale_log2, bf16_t* __restrict__ out) {
+  constexpr int HD = 128;
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[DMA_RING * DMA_CHUNK_BYTES];
+  const int tile = blockIdx.x, kvh = blockIdx.y;
+  const int G = n_q / g.n_kv;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 15, h = lane >> 4;
+  const int b = tiles[3 * tile], q_begin = tiles[3 * tile + 1], q_end = tiles[3 * tile + 2];
+  const int ctx = seq_lens[b];
+  const int qs = q_start[b], qlen = q_start[b + 1] - qs;
+  const int pos0 = ctx - qlen;
+  const int* table = block_tables + static_cast<size_t>(b) * max_blocks;
+  const int kv_end = pos0 + (q_end - 1 - qs) + 1;  // keys visible to the tile's last row
+  const int nchunk = (kv_end + CHUNK - 1) / CHUNK;
+  const int nblk = (kv_end + BS - 1) / BS;
+
+  const int row0 = q_begin + 16 * w;
+  const bool wave_rows = row0 < q_end;  // wave-uniform; idle waves still stage K/V and hit barriers
+  const int my_row = row0 + r;
+  const bool row_ok = my_row < q_end;
+  const int my_pos = pos0 + (my_row - qs);
+  const int first_pos = pos0 + (row0 - qs);
+  const int w_end = wave_rows ? pos0 + (min(row0 + 15, q_end - 1) - qs) + 1 : 0;
+  bf16x8 bq[GT][HD / 32];
+  float m[GT], l[GT];
+  f32x4 o[GT][HD / 16];
+  // GT need not divide G: the heads past G of the last z-group are computed on a clamped
+  // head and never stored
+#pragma unroll
+  for (int gt = 0; gt < GT; ++gt) {
+    const int qh = kvh * G + min(static_cast<int>(blockIdx.z) * GT + gt, G - 1);
+    load_q<HD>(bq[gt], q + (static_cast<size_t>(row_ok ? my_row : (wave_rows ? row0 : q_begin)) * n_q + qh) * HD,
+               row_ok, lane);
+    m[gt] = -INFINITY;
+    l[gt] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) o[gt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Q landed: from here vmcnt counts glds only
+
+  // this lane's source piece of glds i (0..3) of a chunk: waves 0-1 K rows, waves 2-3 V dims
+  auto issue = [&](int c) {
+    uint8_t* slot = smem + (c % DMA_RING) * DMA_CHUNK_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf16_t* src;
+      uint8_t* dst;
+      if (w < 2) {
+        const int t = 16 * w + 4 * i + (lane >> 4);  // chunk token = K image row
+        const int j = (lane & 15) ^ k_swz(t);         // logical 16-B piece stored at slot (lane & 15)
+        const int blk = table[min(2 * c + (t >> 4), nblk - 1)];
+        src = g.k + block_base<HD>(g, blk, kvh) + (t & (BS - 1)) * HD + j * 8;
+        dst = slot + (16 * w + 4 * i) * 256;
+      } else {
+        const int d = 64 * (w - 2) + 16 * i + (lane >> 2);  // V^T image row
+        const int hh = (lane & 3) ^ ((d >> 2) & 3);
+        const int blk = table[min(2 * c + (hh >> 1), nblk - 1)];
+        src = g.v + block_base<HD>(g, blk, kvh) + d * BS + (hh & 1) * 8;
+        dst = slot + LDS_K_BYTES + (64 * (w - 2) + 16 * i) * 64;
+      }
+      __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+    }
+  };
+
+  constexpr int LEAD = DMA_RING - 1;  // chunks in flight ahead of the one computed
+  static_assert(LEAD >= 1 && LEAD <= 4, "ring depth");
+#pragma unroll
+  for (int i = 0; i < LEAD; ++i)
+    if (i < nchunk) issue(i);
+  // one barrier per chunk for every wave: wait for chunk c, barrier, refill the freed slot
+  auto sync_issue = [&](int c) {
+    const int younger = min(LEAD - 1, nchunk - 1 - c);  // chunks issued after c, still allowed in flight
+    if (younger >= 3) {
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    } else if (younger == 2) {
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else if (younger == 1) {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + LEAD < nchunk) issue(c + LEAD);  // into the slot of chunk c - 1: every wave is past its reads
+  };
+  auto read_chunk = [&](int c, Chunk<HD>& ch) {
+    const uint8_t* kimg = smem + (c % DMA_RING) * DMA_CHUNK_BYTES;
+    const uint8_t* vimg = kimg + LDS_K_BYTES;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = 8 * (r >> 2) + 4 * u + (r & 3);
+#pragma unroll
+      for (int kk = 0; kk < HD / 32; ++kk)
+        ch.k[u][kk] = *reinterpret_cast<const bf16x8*>(kimg + t * 256 + (((kk * 4 + h) ^ k_swz(t)) << 4));
+    }
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) {
+      const int d = dt * 16 + r;
+      ch.v[dt] = *reinterpret_cast<const bf16x8*>(vimg + d * 64 + ((h ^ ((d >> 2) & 3)) << 4));
+    }
+  };
+  // chunks every row of this wave sees in full: the GT heads as one straight-line block
+  // (full_scores / full_pv, as the NT sub-tiles of the register kernel), the lazy O rescale
+  // outside the inner loop; the wave's diagonal chunks and the rest of the tile afterwards
+  const int n_full = wave_rows ? min(first_pos / CHUNK, nchunk) : 0;
+  auto none = [](Chunk<HD>&) {};
+  int c = 0;
+  while (c < n_full) {
+    f32x4 sc[GT][2];
+    float mx[GT];
+    Chunk<HD> ch;
+    bool grow = false;
+    for (; c < n_full; ++c) {
+      sync_issue(c);
+      read_chunk(c, ch);
+      grow = full_scores<HD, GT, false>(ch, bq, scale_log2, m, sc, mx, none);
+      if (grow) break;  // wave-uniform
+      full_pv<HD, GT, false>(ch, sc, scale_log2, m, l, o, none);
+    }
+    if (!grow) break;
+    full_rescale<HD, GT>(mx, m, l, o);
+    full_pv<HD, GT, false>(ch, sc, scale_log2, m, l, o, none);
+    ++c;
+  }
+  for (; c < nchunk; ++c) {
+    sync_issue(c);
+    if (wave_rows && c * CHUNK < w_end) {  // wave-uniform
+      Chunk<HD> ch;
+      read_chunk(c, ch);
+#pragma unroll
+      for (int gt = 0; gt < GT; ++gt)
+        compute_chunk<HD, Causal, true, false, DMA_LAZY>(ch, bq[gt], c * CHUNK, w_end, Causal{my_pos}, scale_log2,
+                                                         m[gt], l[gt], o[gt], lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (!row_ok) return;
+#pragma unroll
+  for (int gt = 0; gt < GT; ++gt) {
+    if (static_cast<int>(blockIdx.z) * GT + gt >= G) break;
+    const int qh = kvh * G + blockIdx.z * GT + gt;
+    const float inv = l[gt] > 0.f ? 1.f / l[gt] : 0.f;
+    bf16_t* orow = out + (static_cast<size_t>(my_row) * n_q + qh) * HD;
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) {
+      u16x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = f2bf(o[gt][dt][i] * inv);
+      *reinterpret_cast<u16x4*>(orow + dt * 16 + 4 * h) = v;
+    }
+  }
+}
+
 // heads per workgroup for the LDS kernel: the largest divisor of G that is <= 5
 inline int lds_group_tile(int G) {
   for (int gt = 5; gt >= 1; --gt)
@@ -848,14 +1028,26 @@ inline int lds_group_tile(int G) {
 
 int launch_prefill_lds(int n_tiles, int n_q, int n_kv, const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
                        const int* q_start, const int* seq_lens, const int* tiles, float sl, bf16_t* out,
-                       hipStream_t stream) {
-  const int G = n_q / n_kv, gt = lds_group_tile(G);
-  const dim3 grid(n_tiles, n_kv, G / gt);
+                       hipStream_t stream, bool dma = false) {
+  const int G = n_q / n_kv;
+  int gt = lds_group_tile(G);
+  if (dma) {  // heads per workgroup of the glds kernel (BCG_PREFILL_GT, default min(G, 5))
+    static const int env_gt = [] {
+      const char* e = std::getenv("BCG_PREFILL_GT");
+      return e ? std::atoi(e) : 0;
+    }();
+    gt = env_gt >= 1 && env_gt <= 5 ? env_gt : std::min(G, 5);
+  }
+  const dim3 grid(n_tiles, n_kv, (G + gt - 1) / gt);
   switch (gt) {
 #define BCG_LDS_CASE(GT)                                                                                         \
   case GT:                                                                                                       \
-    hipLaunchKernelGGL(prefill_attn_lds_kernel<GT>, grid, dim3(256), 0, stream, q, g, tables, max_blocks,      \
-                       q_start, seq_lens, tiles, n_q, sl, out);                                                  \
+    if (dma)                                                                                                     \
+      hipLaunchKernelGGL(prefill_attn_dma_kernel<GT>, grid, dim3(256), 0, stream, q, g, tables, max_blocks,    \
+                         q_start, seq_lens, tiles, n_q, sl, out);                                                \
+    else                                                                                                         \
+      hipLaunchKernelGGL(prefill_attn_lds_kernel<GT>, grid, dim3(256), 0, stream, q, g, tables, max_blocks,    \
+                         q_start, seq_lens, tiles, n_q, sl, out);                                                \
     break;
     BCG_LDS_CASE(1)
     BCG_LDS_CASE(2)
@@ -969,10 +1161,10 @@ BCG_API int bcg_paged_attention_prefill(const void* q, const void* k_cache, cons
   const bf16_t* qb = static_cast<const bf16_t*>(q);
   bf16_t* ob = static_cast<bf16_t*>(out);
   int rc;
-  if (nt == 0 && !(hd == 128 && !kv_fp8)) nt = 4;
-  if (nt == 0)  // LDS-shared K/V variant
+  if ((nt == 0 || nt == 8) && !(hd == 128 && !kv_fp8)) nt = 4;
+  if (nt == 0 || nt == 8)  // LDS-shared K/V: 0 = register-staged, 8 = glds ring
     rc = launch_prefill_lds(n_tiles, n_q, n_kv, qb, g, block_tables, max_blocks, q_start, seq_lens, tiles, sl, ob,
-                            stream);
+                            stream, nt == 8);
   else if (hd == 128)
     rc = kv_fp8 ? launch_prefill<128, true>(nt, n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens,
                                             tiles, sl, ob, stream)

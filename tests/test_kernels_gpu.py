@@ -148,7 +148,7 @@ def _prefill_tiles(q_start, seq_lens):
 
 
 @pytest.mark.parametrize("nt,kv_dtype", [(1, torch.bfloat16), (2, torch.bfloat16), (4, torch.bfloat16), (4, F8),
-                                         (0, torch.bfloat16)])
+                                         (0, torch.bfloat16), (8, torch.bfloat16)])
 @pytest.mark.parametrize("n_q,n_kv,hd", [(40, 8, 128), (14, 2, 64), (48, 8, 128), (64, 8, 128), (32, 8, 128)])
 def test_paged_attention_prefill(hip, n_q, n_kv, hd, nt, kv_dtype):
     gen = torch.Generator().manual_seed(3)
