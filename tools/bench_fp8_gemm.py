@@ -37,13 +37,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="mistral-22b")
     ap.add_argument("--ms", default="32,64,128,160,256,320,512")
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree of the shard shapes")
     args = ap.parse_args()
     cfg = get_model_config(args.model)
     hip = get_ops("hip")
-    H, I = cfg.hidden_size, cfg.intermediate_size
+    H, I, tp = cfg.hidden_size, cfg.intermediate_size // args.tp, args.tp
     hd = cfg.head_dim or H // cfg.num_heads
-    shapes = {"qkv": ((cfg.num_heads + 2 * cfg.num_kv_heads) * hd, H), "o": (H, cfg.num_heads * hd),
-              "gate_up": (2 * I, H), "down": (H, I)}
+    nq, nkv = cfg.num_heads // tp, cfg.num_kv_heads // tp
+    shapes = {"qkv": ((nq + 2 * nkv) * hd, H), "o": (H, nq * hd), "gate_up": (2 * I, H), "down": (H, I)}
     out = {}
     for name, (N, K) in shapes.items():
         copies = max(2, int(1.2e9 // (N * K)))
@@ -78,7 +79,7 @@ def main():
                   f"({tf:6.0f} TF/s, x{res['lib'] / best[0]:4.2f})", flush=True)
             out[f"{M},{N},{K}"] = {k: round(v, 2) for k, v in res.items()}
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "bench_fp8_gemm.json"), "w") as fh:
+    with open(os.path.join(ROOT, "gpurun_out", f"bench_fp8_gemm_tp{args.tp}.json"), "w") as fh:
         json.dump(out, fh, indent=1)
 
 
