@@ -94,8 +94,10 @@ ENGINE_CONFIG = {
     "honor_max_num_seqs": False,
     "kv_cache_gb": None,           # None = size from gpu_memory_utilization
     "kv_cache_dtype": os.environ.get("BCG_KV_CACHE_DTYPE", "auto"),  # auto (bf16) | fp8 (e4m3fn)
-    # decode bursts a prompt may wait so prefill runs in full chunks (0 = admit immediately)
-    "admit_max_wait": int(os.environ.get("BCG_ADMIT_MAX_WAIT", "0")),
+    # decode bursts a prompt may wait so prefill runs in full chunks (0 = admit immediately);
+    # only while >= admit_min_live rows decode.  3 vs 0, two A/B pairs on one GPU: 31.0k / 31.5k
+    # vs 30.6k / 30.8k tokens/s (profiles/bench_r2_ab*_a*.json)
+    "admit_max_wait": int(os.environ.get("BCG_ADMIT_MAX_WAIT", "3")),
     # prefill on a second HIP stream, overlapped with decode bursts (single-GPU / DP ranks).
     # Off by default: measured no gain at 32 sims/GPU (19.2 vs 19.1 decisions/s), and
     # hipBLASLt's stream-K prefill GEMMs (inter-workgroup waits) beside a second
