@@ -299,12 +299,19 @@ def hip_ops() -> SimpleNamespace:
             return silu_mul(linear(x, w))
         return gemm_nt(x, w, cfg, 1)
 
+    residual_addmm = os.environ.get("BCG_RESIDUAL_ADDMM", "1") == "1"
+
     def linear_residual(x, w, residual):
         """residual <- residual + x W^T (in place; the o/down projection fused with the
         residual-stream update of the next add+RMSNorm).  Returns `residual`."""
         M, K = x.shape
         cfg = plan.choose(M, w.shape[0], K, 2) if x.is_contiguous() and x.dtype == torch.bfloat16 else None
         if cfg is None:
+            if (residual_addmm and residual.is_contiguous() and residual.dtype == x.dtype == w.dtype
+                    and residual.shape == (M, w.shape[0])):
+                # hipBLASLt with beta = 1: the residual add rides in the GEMM epilogue (one read
+                # of the residual, no separate elementwise pass over three [M, H] tensors)
+                return residual.addmm_(x, w.t())
             residual.add_(linear(x, w))
             return residual
         return gemm_nt(x, w, cfg, 2, residual=residual, out=residual)
