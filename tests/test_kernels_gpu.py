@@ -74,6 +74,30 @@ def test_qk_norm_rope_kv_write(hip, n_q, n_kv, hd, qk_norm, kv_dtype):
         _close(v2, v1, atol=0, rtol=0)
 
 
+@pytest.mark.parametrize("hd,n_q,n_kv", [(128, 40, 8), (64, 14, 2)])
+def test_qk_norm_rope_kv_write_prefill_groups(hip, hd, n_q, n_kv):
+    """Prefill-sized T (>= 64): V goes through the grouped writer -- whole in-order blocks as
+    32-B rows, everything else (mid-block starts, sequence boundaries, a partial last group)
+    element by element."""
+    torch.manual_seed(4)
+    L, NB = 2, 40
+    # sequence A: 100 tokens from the start of block 2; sequence B: 70 tokens from block 20 offset 5
+    slots = torch.cat([torch.arange(32, 132), torch.arange(20 * 16 + 5, 20 * 16 + 75)]).to(torch.int32).cuda()
+    T = slots.numel()
+    qkv = torch.randn(T, (n_q + 2 * n_kv) * hd, device="cuda", dtype=torch.bfloat16)
+    pos = torch.cat([torch.arange(100), torch.arange(5, 75)]).to(torch.int32).cuda()
+    qn = (torch.rand(hd, device="cuda") + 0.5).to(torch.bfloat16)
+    kn = (torch.rand(hd, device="cuda") + 0.5).to(torch.bfloat16)
+    cs = R.rope_cache(8192, hd, 1e6, "cuda")
+    k1, v1 = _caches(L, NB, n_kv, hd, fill=False)
+    k2, v2 = _caches(L, NB, n_kv, hd, fill=False)
+    q_ref = R.qk_norm_rope_kv_write(qkv, pos, slots, n_q, n_kv, hd, qn, kn, 1e-6, cs, k1, v1, 1)
+    q = hip.qk_norm_rope_kv_write(qkv, pos, slots, n_q, n_kv, hd, qn, kn, 1e-6, cs, k2, v2, 1)
+    _close(q, q_ref, atol=3e-2)
+    _close(k2, k1, atol=3e-2)
+    assert torch.equal(v2, v1)
+
+
 def _tables(B, lens, NB, max_blocks, gen):
     perm = torch.randperm(NB - 1, generator=gen) + 1
     tables = torch.zeros(B, max_blocks, dtype=torch.int32)
