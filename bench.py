@@ -66,6 +66,11 @@ def parse(argv=None):
                     help="decode batch cap (rows); default ENGINE_CONFIG['max_batch_seqs']")
     ap.add_argument("--ramp-s", type=float, default=None,
                     help="start the games spread over this many seconds (default: half the warmup)")
+    ap.add_argument("--age-p", type=float, default=0.2,
+                    help="age-diverse pool: each slot's first game is burned in for A ~ Geometric(p) rounds "
+                         "(scripted CPU engine, before any timed window); 0 = every game starts fresh")
+    ap.add_argument("--burnin-chars", default="400,200",
+                    help="internal_strategy,public_reasoning characters of the burn-in outputs")
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--max-rounds", type=int, default=50)
     ap.add_argument("--seed", type=int, default=1234)
@@ -120,10 +125,55 @@ class SimPool:
         self.sims = [self._new_sim(i) for i in range(n_sims)]
         self.retired = 0          # accepted decisions of games already replaced
         self.games_finished = 0
+        self.game_rounds = []     # rounds played by each finished game (burn-in rounds included)
+        self.ages = [0] * n_sims  # burn-in rounds of each slot's first game
         self.outcomes = {}
         self.errors = []
         self._stop = threading.Event()
         self.threads = []
+
+    def burn_in(self, p: float, seed: int, strategy_chars: int, reasoning_chars: int):
+        """Age-diverse start: slot i's first game plays A_i ~ Geometric(p) rounds (support
+        0, 1, 2, ...; capped below max_rounds) on a scripted CPU engine before the pool
+        starts.  In a pool that has run for a long time a slot's game age is distributed
+        as P(age >= a) = P(game length > a); with a per-round stop probability p that is
+        this geometric law, so the timed windows see the round mix of whole games
+        instead of every game in its first rounds at once.  Burn-in decisions are not
+        counted (the counters are reset) and happen before warmup."""
+        from byzantine_consensus_llm_agents_amd.engine.fake import BurnInLLM
+        if p <= 0:
+            return
+        rng = random.Random(seed * 7919 + 17)
+        fake = BurnInLLM(strategy_chars, reasoning_chars, seed)
+        for i, sim in enumerate(self.sims):
+            a = 0
+            while rng.random() > p and a < self.max_rounds - 1:
+                a += 1
+            llms = {aid: ag.llm for aid, ag in sim.agents.items()}
+            for ag in sim.agents.values():
+                ag.llm = fake
+            for _ in range(a):
+                if sim.game.game_over:
+                    break
+                sim.run_round()
+            for aid, ag in sim.agents.items():
+                ag.llm = llms[aid]
+            for k in sim.counters:
+                sim.counters[k] = 0
+            self.ages[i] = a
+
+    def output_chars(self):
+        """Mean public_reasoning / internal_strategy characters of the agents' latest outputs."""
+        reason, strat = [], []
+        with self.lock:
+            for sim in self.sims:
+                for ag in sim.agents.values():
+                    reason.append(len(getattr(ag, "last_reasoning", "") or ""))
+                    hist = getattr(ag.state, "last_k_internal_strategies", None)
+                    if hist:
+                        strat.append(len(hist[-1][1] if isinstance(hist[-1], tuple) else str(hist[-1])))
+        mean = lambda v: round(sum(v) / len(v), 1) if v else None  # noqa: E731
+        return {"public_reasoning": mean(reason), "internal_strategy": mean(strat)}
 
     def _new_sim(self, slot):
         seed = self.seed_base + slot * 1_000_003 + self.generation[slot]
@@ -154,6 +204,7 @@ class SimPool:
                     with self.lock:
                         self.outcomes[o] = self.outcomes.get(o, 0) + 1
                         self.games_finished += 1
+                        self.game_rounds.append(min(sim.game.current_round, sim.game.max_rounds))
                         self.retired += self._made(sim)
                         self.sims[i] = fresh
         except BaseException as exc:  # surfaced by the main thread
@@ -262,6 +313,12 @@ def main(argv=None):
     if llm.is_driver:
         llm.start_continuous_batching()
         pool = SimPool(args.sims_per_gpu, args.honest, args.byzantine, args.max_rounds, args.seed, replica)
+        sc, rc = (int(x) for x in args.burnin_chars.split(","))
+        t_b = time.perf_counter()
+        pool.burn_in(args.age_p, args.seed + replica, sc, rc)
+        if rank == 0:
+            print(f"[burn-in] ages {sum(pool.ages) / len(pool.ages):.2f} rounds mean, max {max(pool.ages)} "
+                  f"({time.perf_counter() - t_b:.1f}s)", file=sys.stderr, flush=True)
         ramp = args.ramp_s if args.ramp_s is not None else 0.5 * args.warmup * args.window_s
         pool.start(ramp_s=ramp)
     else:
@@ -348,6 +405,15 @@ def main(argv=None):
             "detail": {"decisions": total_decisions, "elapsed_s": round(elapsed, 3), "init_s": round(init_s, 1),
                        "steps_requested": args.steps, "window_s": args.window_s,
                        "decisions_per_window_rank0": per_window,
+                       "first5_vs_last5": [round(sum(per_window[:5]) / max(1, len(per_window[:5])), 1),
+                                           round(sum(per_window[-5:]) / max(1, len(per_window[-5:])), 1)],
+                       "age_mix": {"p": args.age_p, "burnin_chars": args.burnin_chars,
+                                   "mean_burnin_rounds": (round(sum(pool.ages) / len(pool.ages), 2)
+                                                          if pool else None),
+                                   "mean_rounds_per_finished_game": (
+                                       round(sum(pool.game_rounds) / len(pool.game_rounds), 2)
+                                       if pool and pool.game_rounds else None),
+                                   "output_chars": pool.output_chars() if pool else None},
                        "engine_per_rank": d_eng, "games_finished_rank0": pool.games_finished if pool else 0,
                        "outcomes_rank0": pool.outcomes if pool else {},
                        "wall_since_start_s": round(time.perf_counter() - t_origin, 1),

@@ -119,13 +119,6 @@ def run_concurrently(engine_agent, jobs):
     errors = []
 
     parent_key = getattr(threading.current_thread(), "_bcg_order_key", ())
-    # A participating parent hands its registration to the children and gets it back
-    # from the LAST child to finish (that child does not unregister): the coalescer's
-    # participant count never drops below the threads that will still submit, so a
-    # batch is never flushed without the parent's next ticket.
-    parent = getattr(threading.current_thread(), "_bcg_participant", False)
-    remaining = [len(jobs)]
-    lock = threading.Lock()
 
     def work(i, job):
         threading.current_thread()._bcg_order_key = tuple(parent_key) + (i,)
@@ -134,14 +127,10 @@ def run_concurrently(engine_agent, jobs):
         except BaseException as exc:
             errors.append(exc)
         finally:
-            with lock:
-                remaining[0] -= 1
-                last = remaining[0] == 0
-            if not (parent and last):
-                llm.unregister_client()
+            llm.unregister_client()
 
-    for _ in range(len(jobs) - (1 if parent else 0)):
-        llm.register_client()  # (+ the parent's own registration, handed over)
+    for _ in range(len(jobs)):
+        llm.register_client()
     threads = [threading.Thread(target=work, args=(i, j)) for i, j in enumerate(jobs)]
     for t in threads:
         t.start()

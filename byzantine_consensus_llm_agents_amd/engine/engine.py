@@ -203,8 +203,15 @@ class InferenceEngine:
         # collectives of one communicator must not run on two streams at once.
         self.overlap = bool(args.overlap_prefill and self.device.type == "cuda" and self.tp.size == 1)
         self.prefill_stream = torch.cuda.Stream(self.device) if self.overlap else None
+        if hasattr(self.ops, "prepare_device"):  # split-K counters: allocated before any graph capture
+            self.ops.prepare_device(self.device)
+            if self.prefill_stream is not None:
+                self.ops.register_stream(self.prefill_stream)
+        self._saved_avoid_library = None
         if self.overlap and hasattr(self.ops, "gemm_plan"):
-            # no stream-K library GEMM may run beside the other stream's kernels (ops/gemm_plan.py)
+            # no stream-K library GEMM may run beside the other stream's kernels (ops/gemm_plan.py);
+            # the ops namespace is process-wide: restored by shutdown()
+            self._saved_avoid_library = self.ops.gemm_plan.avoid_library
             self.ops.gemm_plan.avoid_library = True
         self._inflight = None
         self._bursts = 0         # decode bursts launched (admission-batching clock)
@@ -310,10 +317,10 @@ class InferenceEngine:
             "done": torch.ones(cap, dtype=torch.int32, device=dev), "next_tokens": z(),
             "out_tokens": torch.zeros(cap, OUT_WIDTH, dtype=torch.int32, device=dev)}
         self.slots: List[Optional[_Request]] = [None] * cap
-        # one split-K scratch for every decode graph (they never run concurrently)
+        # one split-K scratch for every decode graph (they never run concurrently); every
+        # partial is written before it is read, so no initialisation is needed
         ws = self._decode_ws_bytes() // 4
-        # zeros: the tail holds the decode kernel's split arrival counters (self-resetting)
-        self.decode_ws = torch.zeros(ws, dtype=torch.float32, device=dev) if ws else None
+        self.decode_ws = torch.empty(ws, dtype=torch.float32, device=dev) if ws else None
 
     def _phys(self, blocks: List[int]) -> List[int]:
         return [b + 1 for b in blocks]  # manager ids are shifted past scratch block 0
@@ -416,8 +423,21 @@ class InferenceEngine:
                         self._stop = True
                         self._fatal = exc
                         break
-            if self.tp.size > 1 and self._fatal is None:
-                self._send_plan({"stop": True})
+            if self.tp.size > 1:
+                self._release_followers()
+
+    def _release_followers(self):
+        """Tell the TP followers to leave their plan loop.  After a failed iteration this is
+        best-effort (a follower may be stuck in a collective of that iteration); the error
+        rides along so a follower that does receive it raises instead of exiting cleanly."""
+        msg = {"stop": True}
+        if self._fatal is not None:
+            msg["error"] = f"{type(self._fatal).__name__}: {self._fatal}"
+        try:
+            self._send_plan(msg)
+        except Exception:  # noqa: BLE001 -- the control group itself may be gone
+            if self._fatal is None:
+                raise
 
     def _fail_all(self, exc):
         self._inflight = None
@@ -470,6 +490,8 @@ class InferenceEngine:
             while True:
                 plan = self._recv_plan()
                 if plan.get("stop"):
+                    if plan.get("error"):
+                        raise RuntimeError(f"TP driver failed: {plan['error']}")
                     return
                 self._iterate(plan)
 
@@ -871,11 +893,14 @@ class InferenceEngine:
                 self._cv.notify_all()
             self._thread.join(timeout=120)  # the TP driver's loop sends the followers' stop
             self.async_mode = False
-        elif self.tp.size > 1 and self.is_driver and self.model is not None and self._fatal is None:
-            self._send_plan({"stop": True})  # sync-mode driver: release the followers
+        elif self.tp.size > 1 and self.is_driver and self.model is not None:
+            self._release_followers()  # sync-mode driver
         if self._follower is not None:
             self._follower.join(timeout=120)
             self._follower = None
+        if self._saved_avoid_library is not None:
+            self.ops.gemm_plan.avoid_library = self._saved_avoid_library
+            self._saved_avoid_library = None
         self.graphs = None
         self.k_cache = self.v_cache = None
         self.model = None

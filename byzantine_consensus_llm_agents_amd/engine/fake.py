@@ -182,3 +182,51 @@ class FakeBackend:
 
     def shutdown(self):
         pass
+
+
+class BurnInLLM:
+    """Scripted stand-in for :class:`..engine.llm.LLM` used to AGE games before a benchmark.
+
+    ``bench.py`` plays the first rounds of each pool slot's first game with it (CPU
+    only, before any timed window), so the timed windows see games of every age --
+    as a long-running pool does -- instead of a synchronized fresh start.  Outputs are
+    schema-valid (:func:`scripted_object`) with free-text fields padded to the lengths
+    the real engine produces (``strategy_chars`` / ``reasoning_chars``; the agents clip
+    them to 400 / 600 characters), and every vote is ``continue`` so no game ends
+    during burn-in.
+    """
+
+    def __init__(self, strategy_chars: int = 400, reasoning_chars: int = 200, seed: int = 0):
+        self.strategy_chars, self.reasoning_chars, self.seed = strategy_chars, reasoning_chars, seed
+        self.calls = 0
+
+    @staticmethod
+    def _text(rng: random.Random, n: int) -> str:
+        out = []
+        while sum(len(w) + 1 for w in out) < n:
+            out.append(rng.choice(_WORDS))
+        return " ".join(out)[:n]
+
+    def _answer(self, prompt: str, schema: Optional[Dict]) -> str:
+        obj = scripted_object(prompt, schema, self.seed)
+        if "decision" in obj:
+            obj["decision"] = "continue"
+        else:
+            rng = _rng(prompt, schema, self.seed + 1)
+            if "internal_strategy" in obj:
+                obj["internal_strategy"] = self._text(rng, self.strategy_chars)
+            if "public_reasoning" in (schema or {}).get("properties", {}):
+                obj["public_reasoning"] = self._text(rng, self.reasoning_chars)
+        return json.dumps(obj)
+
+    def generate(self, prompts, sampling_params=None, use_tqdm: bool = False):
+        from .llm import CompletionOutput, RequestOutput
+        if isinstance(prompts, str):
+            prompts = [prompts]
+        params = sampling_params if isinstance(sampling_params, (list, tuple)) else [sampling_params] * len(prompts)
+        self.calls += 1
+        outs = []
+        for i, (p, sp) in enumerate(zip(prompts, params)):
+            schema = sp.guided_decoding.json if sp is not None and sp.guided_decoding is not None else None
+            outs.append(RequestOutput(i, p, [CompletionOutput(0, self._answer(p, schema))]))
+        return outs

@@ -10,7 +10,8 @@ are timed and the fastest is kept).  Shapes the table does not cover use a
 simple rule (hand kernel up to ``max_m`` rows).
 
 ``BCG_HAND_GEMM``: ``0`` = library only, ``1`` (default) = table / rule,
-``force`` = hand kernel wherever the shape is supported (tests).
+``force`` = hand kernel wherever the shape is supported (tests; ``BCG_HAND_GEMM_SPLIT``
+= the split-K to force with it).
 
 ``avoid_library`` (set by the engine when prefill overlaps decode on a second
 stream): every supported shape runs a hand kernel -- the fastest measured hand
@@ -38,6 +39,7 @@ SPLITS = (1, 2, 3, 4, 6, 8)
 class GemmPlan:
     def __init__(self, lib=None, table: Optional[str] = TABLE, max_m: int = 1024):
         self.mode = os.environ.get("BCG_HAND_GEMM", "1")
+        self.force_split = int(os.environ.get("BCG_HAND_GEMM_SPLIT", "1"))  # split-K in "force" mode (tests)
         self.max_m = max_m
         self.avoid_library = False
         self.timings: Dict[Tuple[int, int, int, int], Dict[str, float]] = {}
@@ -96,8 +98,9 @@ class GemmPlan:
             return self._best_hand(M, N, K, epi)
         if self.mode == "force":
             for cfg in (self.default_cfg(M),) + tuple(range(N_CFGS)):
-                if self.supported(cfg, M, N, K, epi):
-                    return (cfg, 1)
+                for split in ((self.force_split, 1) if self.force_split > 1 else (1,)):
+                    if self.supported(cfg, M, N, K, epi, split):
+                        return (cfg, split)
             return None
         choice = self.table.get((M, N, K, epi))
         if choice is None and self.table:  # nearest measured M above (same projection shape)

@@ -43,11 +43,6 @@ def load_library(path: str = None) -> ctypes.CDLL:
                                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                                         c_void_p, c_int, c_int, c_void_p],
         "bcg_decode_split_tokens": [c_int, c_int, c_int],
-        "bcg_paged_attention_decode_exp": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
-                                           c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_int, c_int,
-                                           c_void_p, c_int, c_void_p],
-        "bcg_gemm_skinny": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                            c_void_p],
         "bcg_quant_fp8": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
         "bcg_add_rmsnorm_fp8": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_int,
                                 c_void_p],
@@ -187,23 +182,8 @@ def hip_ops() -> SimpleNamespace:
             "paged_attention_decode")
         return out
 
-    def paged_attention_decode_exp(q, k_cache, v_cache, layer, block_tables, seq_lens, scale, variant):
-        """Timing-only kernel variants (tools/bench_ops.py); not numerically valid for the engine."""
-        B, n_q, hd = q.shape
-        L, NB, n_kv, BS, _ = k_cache.shape
-        max_blocks = block_tables.shape[1]
-        max_splits = (max_blocks * BS + 127) // 128
-        ws = torch.empty(B * n_q * max_splits * (hd + 2), dtype=torch.float32, device=q.device)
-        out = torch.empty(B, n_q * hd, dtype=q.dtype, device=q.device)
-        _check(lib.bcg_paged_attention_decode_exp(
-            _p(q), _p(k_cache), _p(v_cache), layer, NB, n_kv, _p(block_tables), max_blocks, _p(seq_lens),
-            B, n_q, hd, scale, _p(ws), max_splits, 128, _p(out), variant, _stream()), "decode_exp")
-        return out
-
-    prefill_nt = int(os.environ.get("BCG_PREFILL_NT", "4"))  # 16-row query tiles per wave
-
     def paged_attention_prefill(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale,
-                                max_q_len=None, tiles=None, nt=None):
+                                max_q_len=None, tiles=None):
         T, n_q, hd = q.shape
         L, NB, n_kv, BS, _ = k_cache.shape
         _req(tiles is not None and tiles.dtype == torch.int32 and tiles.dim() == 2 and tiles.shape[1] == 3,
@@ -214,48 +194,59 @@ def hip_ops() -> SimpleNamespace:
         _check(lib.bcg_paged_attention_prefill(
             _p(q), _p(k_cache), _p(v_cache), layer, NB, n_kv, _p(block_tables), block_tables.shape[1],
             _p(q_start), _p(seq_lens), _p(tiles), tiles.shape[0], n_q, hd, BS, scale, _p(out),
-            prefill_nt if nt is None else nt, _kv_fp8(k_cache, v_cache), _stream()), "paged_attention_prefill")
+            4, _kv_fp8(k_cache, v_cache), _stream()), "paged_attention_prefill")
         return out
 
-    use_skinny = os.environ.get("BCG_SKINNY_GEMM", "0") == "1"  # hipBLASLt wins (bench_ops r1)
-    skinny_max_m = int(os.environ.get("BCG_SKINNY_MAX_M", "192"))
-
-    def skinny_split(N: int, K: int) -> int:
-        nblocks = N // 128
-        ksteps = K // 32
-        # aim for ~2 workgroups per CU, keep >= 8 k-steps (256 of K) per split
-        return max(1, min(512 // nblocks, ksteps // 8))
-
     def linear(x, w, bias=None):
-        """y = x W^T (+b): hand MFMA GEMM where the plan says it beats hipBLASLt (decode
-        shapes), the optional skinny weight-streaming kernel, hipBLASLt otherwise."""
+        """y = x W^T (+b): hand MFMA GEMM where the plan says it beats hipBLASLt, hipBLASLt otherwise."""
         M, K = x.shape
         N = w.shape[0]
         if x.is_contiguous() and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
             cfg = plan.choose(M, N, K, 0)
             if cfg is not None:
                 return gemm_nt(x, w, cfg, 0, bias=bias)
-        if not (use_skinny and M <= skinny_max_m and N % 128 == 0 and K % 128 == 0 and x.is_contiguous()
-                and w.is_contiguous() and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
-            return torch.nn.functional.linear(x, w, bias)
-        _req(w.shape[1] == K and (bias is None or bias.shape == (N,)), "linear shapes")
-        split = skinny_split(N, K)
-        y = torch.empty(M, N, dtype=x.dtype, device=x.device)
-        ws = torch.zeros(M, N, dtype=torch.float32, device=x.device) if split > 1 else None
-        _check(lib.bcg_gemm_skinny(_p(x), _p(w), _p(bias) if bias is not None else None, _p(y),
-                                   _p(ws) if ws is not None else None, M, N, K, split, _stream()), "gemm_skinny")
-        return y
+        return torch.nn.functional.linear(x, w, bias)
 
     from .gemm_plan import GemmPlan
     plan = GemmPlan(lib)
 
-    counters = {}  # per (device, stream): split-K arrival counters, zero between launches
+    # Split-K arrival counters (one int per output tile; the last-arriving workgroup of a
+    # tile resets its counter, so a buffer stays zero between launches).  Kernels that may
+    # run CONCURRENTLY need disjoint buffers: one per device for the engine's main stream --
+    # shared by eager launches and every captured decode graph, which replay on that stream
+    # one after another -- and one per registered side stream (the overlapped-prefill
+    # stream).  Buffers are allocated eagerly by `prepare_device` / `register_stream`, never
+    # inside a graph capture: a zero-fill captured into one bucket's graph would leave the
+    # buffer uninitialised for every other graph (ADVICE r2).
+    counters = {}       # device index -> int32 [65536]
+    side_counters = {}  # (device index, stream handle) -> int32 [65536]
+
+    def _new_counters(dev):
+        _req(not torch.cuda.is_current_stream_capturing(),
+             "split-K counters must be allocated outside graph capture (ops.prepare_device)")
+        return torch.zeros(1 << 16, dtype=torch.int32, device=dev)
+
+    def prepare_device(dev):
+        dev = torch.device(dev)
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        if dev.index not in counters:
+            counters[dev.index] = _new_counters(dev)
+
+    def register_stream(stream):
+        """Give `stream` its own split-K counters (its GEMMs may overlap the main stream's)."""
+        key = (stream.device.index, stream.cuda_stream)
+        if key not in side_counters:
+            side_counters[key] = _new_counters(stream.device)
 
     def _counters(dev):
-        key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
-        if key not in counters:
-            counters[key] = torch.zeros(1 << 16, dtype=torch.int32, device=dev)
-        return counters[key]
+        dev = torch.device("cuda", dev.index if dev.index is not None else torch.cuda.current_device())
+        side = side_counters.get((dev.index, torch.cuda.current_stream(dev).cuda_stream))
+        if side is not None:
+            return side
+        if dev.index not in counters:
+            prepare_device(dev)  # raises under capture
+        return counters[dev.index]
 
     def gemm_nt(x, w, cfg, epi=0, bias=None, residual=None, out=None, split_k=1):
         """Hand MFMA GEMM (csrc/kernels/gemm.hip): x [M,K] @ w[N,K]^T with epilogue `epi`
@@ -418,12 +409,13 @@ def hip_ops() -> SimpleNamespace:
                                 out_dtype=out_dtype)
 
     return SimpleNamespace(name="hip", linear=linear, linear_silu=linear_silu, linear_residual=linear_residual,
-                           gemm_nt=gemm_nt, gemm_plan=plan, quant_fp8=quant_fp8, add_rmsnorm_fp8=add_rmsnorm_fp8,
+                           gemm_nt=gemm_nt, gemm_plan=plan, prepare_device=prepare_device,
+                           register_stream=register_stream, quant_fp8=quant_fp8, add_rmsnorm_fp8=add_rmsnorm_fp8,
                            silu_mul_fp8=silu_mul_fp8, linear_fp8=linear_fp8, gemm_nt_fp8=gemm_nt_fp8, fp8_cfg=fp8_cfg, rmsnorm=rmsnorm, add_rmsnorm=add_rmsnorm, silu_mul=silu_mul,
                            embed_rmsnorm=embed_rmsnorm,
                            qk_norm_rope_kv_write=qk_norm_rope_kv_write,
                            paged_attention_decode=paged_attention_decode,
                            decode_workspace_numel=decode_workspace_numel,
                            paged_attention_prefill=paged_attention_prefill,
-                           paged_attention_decode_exp=paged_attention_decode_exp, sample_step=sample_step,
+                           sample_step=sample_step,
                            library=lib)

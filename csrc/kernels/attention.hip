@@ -80,7 +80,7 @@ __device__ __forceinline__ bf16x8 to_bf16x8(const u32x2& x) {  // 8 x e4m3fn -> 
 }
 
 // Issue every load of one 32-token chunk whose blocks are blk0/blk1.
-template <int HD, bool KT = false, bool F8 = false>
+template <int HD, bool F8 = false>
 __device__ __forceinline__ void load_chunk(Chunk<HD, F8>& c, const KVGeom& g, int blk0, int blk1, int kvh,
                                            int lane) {
   typedef typename Chunk<HD, F8>::E E;
@@ -92,10 +92,9 @@ __device__ __forceinline__ void load_chunk(Chunk<HD, F8>& c, const KVGeom& g, in
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int t = 8 * (r >> 2) + 4 * u + (r & 3);
-    // KT: K block-head stored [HD/32][BS][32] -> each load instruction reads 256-B runs
-    const T* krow = kc + (t < BS ? b0 : b1) + (KT ? (t & (BS - 1)) * 32 : (t & (BS - 1)) * HD) + 8 * h;
+    const T* krow = kc + (t < BS ? b0 : b1) + (t & (BS - 1)) * HD + 8 * h;
 #pragma unroll
-    for (int kk = 0; kk < HD / 32; ++kk) c.k[u][kk] = *reinterpret_cast<const E*>(krow + kk * (KT ? BS * 32 : 32));
+    for (int kk = 0; kk < HD / 32; ++kk) c.k[u][kk] = *reinterpret_cast<const E*>(krow + kk * 32);
   }
   const T* vb = vc + (h < 2 ? b0 : b1) + 8 * (h & 1);
 #pragma unroll
@@ -352,7 +351,7 @@ struct Causal {
 // B = 160, ctx 1700, max_model_len 8192.
 constexpr int DEC_MAX_B = 2048;
 
-template <int HD, bool KT = false, bool F8 = false, int CPW = 1>
+template <int HD, bool F8 = false, int CPW = 1>
 __global__ __launch_bounds__(256) void decode_attn_kernel(
     const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
     const int* __restrict__ seq_lens, int B, int n_q, float scale_log2, float* __restrict__ part_o,
@@ -427,7 +426,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
     for (int j = 0; j < CPW; ++j) {
       const int tj = t0 + j * CHUNK;
       if (tj < ctx)  // wave-uniform
-        load_chunk<HD, KT, F8>(c[j], g, table[tj / BS], table[min(tj / BS + 1, last_blk)], kvh, lane);
+        load_chunk<HD, F8>(c[j], g, table[tj / BS], table[min(tj / BS + 1, last_blk)], kvh, lane);
     }
 #pragma unroll
     for (int j = 0; j < CPW; ++j) {
@@ -526,7 +525,7 @@ __global__ __launch_bounds__(64 * COMBINE_WAVES) void decode_combine_kernel(
   for (int e = 0; e < PER; ++e) out[static_cast<size_t>(bq) * HD + lane * PER + e] = f2bf(acc[e] * inv);
 }
 
-template <int HD, bool KT = false, bool F8 = false, int CPW = 1>
+template <int HD, bool F8 = false, int CPW = 1>
 void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks, const int* seq_lens, int B,
                    int n_q, float sl, float* ws, int max_splits, bf16_t* out, hipStream_t stream) {
   constexpr int DEC_SPLIT = DEC_WAVES * CHUNK * CPW;
@@ -538,11 +537,11 @@ void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
     int per_cu = 0, cus = 0, dev = 0;
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_attn_kernel<HD, KT, F8, CPW>, 256, 0);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_attn_kernel<HD, F8, CPW>, 256, 0);
     resident = std::max(1, per_cu) * std::max(1, cus);
   }
   const int grid = static_cast<int>(std::min<long>(static_cast<long>(B) * g.n_kv * max_splits, resident));
-  hipLaunchKernelGGL((decode_attn_kernel<HD, KT, F8, CPW>), dim3(grid), dim3(256), 0, stream, q, g, tables, max_blocks,
+  hipLaunchKernelGGL((decode_attn_kernel<HD, F8, CPW>), dim3(grid), dim3(256), 0, stream, q, g, tables, max_blocks,
                      seq_lens, B, n_q, sl, part_o, part_ml, max_splits);
   const int n_bq = B * n_q;
   hipLaunchKernelGGL(decode_combine_kernel<HD>, dim3((n_bq + COMBINE_WAVES - 1) / COMBINE_WAVES),
@@ -629,7 +628,7 @@ __global__ __launch_bounds__(256) PREFILL_ATTR void prefill_attn_kernel(
   // next-chunk loads issued unconditionally (clamped to the last chunk) -- see decode
   const int nchunk = (kv_end + CHUNK - 1) / CHUNK;
   Chunk<HD, F8> cur;
-  load_chunk<HD, false, F8>(cur, g, block_at(0), block_at(min(1, nblk - 1)), kvh, lane);
+  load_chunk<HD, F8>(cur, g, block_at(0), block_at(min(1, nblk - 1)), kvh, lane);
 #if PREFILL_FULL_BLOCK
   // chunks every row of the wave sees in full: one interleaved block for all NT sub-tiles,
   // the next chunk reloaded in place (K after the S^T MFMAs, V after the P.V MFMAs): no
@@ -665,7 +664,7 @@ __global__ __launch_bounds__(256) PREFILL_ATTR void prefill_attn_kernel(
   for (int c = 0; c < nchunk; ++c) {
 #endif
     const int cn = min(c + 1, nchunk - 1);
-    load_chunk<HD, false, F8>(nxt, g, block_at(2 * cn), block_at(min(2 * cn + 1, nblk - 1)), kvh, lane);
+    load_chunk<HD, F8>(nxt, g, block_at(2 * cn), block_at(min(2 * cn + 1, nblk - 1)), kvh, lane);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       if (c * CHUNK >= sub_end[nt]) continue;  // wave-uniform: chunk wholly in this sub-tile's causal future
@@ -695,393 +694,13 @@ __global__ __launch_bounds__(256) PREFILL_ATTR void prefill_attn_kernel(
   }
 }
 
-// ---- prefill, LDS-shared K/V (bf16 caches, HD = 128) ------------------------
-// A workgroup = one 64-row tile x one kv head x GT of its query heads.  Each
-// 32-token K/V chunk (16 KiB) is loaded ONCE per workgroup -- 4 x 16 B per
-// thread, coalesced 4 KiB block runs -- into a double-buffered, XOR-swizzled
-// LDS image, and all 4 waves (16 rows each) x GT heads read their MFMA
-// operands from it: every global K/V byte feeds 4*GT times the MFMAs of the
-// register-direct kernel above.  Pipeline per chunk: issue the next chunk's
-// global loads -> compute this chunk from LDS -> write the staged registers to
-// the other buffer -> barrier.
-//   K image: row = token (256 B); 16-B column j stored at j ^ swz(t),
-//            swz(t) = (t ^ (t >> 4)) & 15: the 16 rows one MFMA fragment
-//            gathers land on 16 different bank groups.
-//   V image: row = dim d (64 B = 32 tokens); 16-B column h stored at
-//            h ^ ((d >> 2) & 3): 16 consecutive rows -> 16 bank groups.
-constexpr int LDS_K_BYTES = CHUNK * 128 * 2;   // 8 KiB
-constexpr int LDS_V_BYTES = 128 * CHUNK * 2;   // 8 KiB
-
-__device__ __forceinline__ int k_swz(int t) { return (t ^ (t >> 4)) & 15; }
-
-template <int GT>
-__global__ __launch_bounds__(256) void prefill_attn_lds_kernel(
-    const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
-    const int* __restrict__ q_start, const int* __restrict__ seq_lens, const int* __restrict__ tiles,
-    int n_q, float scale_log2, bf16_t* __restrict__ out) {
-  constexpr int HD = 128;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2][LDS_K_BYTES + LDS_V_BYTES];
-  const int tile = blockIdx.x, kvh = blockIdx.y;
-  const int G = n_q / g.n_kv;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r = lane & 15, h = lane >> 4;
-  const int b = tiles[3 * tile], q_begin = tiles[3 * tile + 1], q_end = tiles[3 * tile + 2];
-  const int ctx = seq_lens[b];
-  const int qs = q_start[b], qlen = q_start[b + 1] - qs;
-  const int pos0 = ctx - qlen;
-  const int* table = block_tables + static_cast<size_t>(b) * max_blocks;
-  const int kv_end = pos0 + (q_end - 1 - qs) + 1;  // keys visible to the tile's last row
-  const int nchunk = (kv_end + CHUNK - 1) / CHUNK;
-  const int nblk = (kv_end + BS - 1) / BS;
-
-  // this wave's 16 rows x GT heads
-  const int row0 = q_begin + 16 * w;
-  const bool wave_rows = row0 < q_end;  // wave-uniform; idle waves still stage K/V and hit barriers
-  const int my_row = row0 + r;
-  const bool row_ok = my_row < q_end;
-  const int my_pos = pos0 + (my_row - qs);
-  const int first_pos = pos0 + (row0 - qs);
-  const int w_end = wave_rows ? pos0 + (min(row0 + 15, q_end - 1) - qs) + 1 : 0;
-  bf16x8 bq[GT][HD / 32];
-  float m[GT], l[GT];
-  f32x4 o[GT][HD / 16];
-#pragma unroll
-  for (int gt = 0; gt < GT; ++gt) {
-    const int qh = kvh * G + blockIdx.z * GT + gt;
-    load_q<HD>(bq[gt], q + (static_cast<size_t>(row_ok ? my_row : (wave_rows ? row0 : q_begin)) * n_q + qh) * HD,
-               row_ok, lane);
-    m[gt] = -INFINITY;
-    l[gt] = 0.f;
-#pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt) o[gt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-
-  // staging: thread tid moves 16-B piece p = tid + 256*i (i < 4) of the chunk:
-  // i = 0,1 -> K (piece = blk_local*256 + token*16 + j), i = 2,3 -> V (blk_local*256 + d*2 + half)
-  u32x4 stage[4];
-  auto issue = [&](int c) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int piece = tid + 256 * (i & 1);
-      const int bl = piece >> 8, within = piece & 255;
-      const int blk = table[min(2 * c + bl, nblk - 1)];
-      const size_t base = block_base<HD>(g, blk, kvh);
-      const bf16_t* src = (i < 2 ? g.k : g.v) + base + within * 8;
-      stage[i] = *reinterpret_cast<const u32x4*>(src);
-    }
-  };
-  auto commit = [&](int buf) {
-    uint8_t* kimg = smem[buf];
-    uint8_t* vimg = smem[buf] + LDS_K_BYTES;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int piece = tid + 256 * (i & 1);
-      const int bl = piece >> 8, within = piece & 255;
-      if (i < 2) {
-        const int t = bl * 16 + (within >> 4), j = within & 15;
-        *reinterpret_cast<u32x4*>(kimg + t * 256 + ((j ^ k_swz(t)) << 4)) = stage[i];
-      } else {
-        const int d = within >> 1, hh = bl * 2 + (within & 1);
-        *reinterpret_cast<u32x4*>(vimg + d * 64 + ((hh ^ ((d >> 2) & 3)) << 4)) = stage[i];
-      }
-    }
-  };
-
-  issue(0);
-  commit(0);
-  __syncthreads();
-  for (int c = 0; c < nchunk; ++c) {
-    const int buf = c & 1;
-    if (c + 1 < nchunk) issue(c + 1);
-    if (wave_rows && c * CHUNK < w_end) {  // wave-uniform
-      const uint8_t* kimg = smem[buf];
-      const uint8_t* vimg = smem[buf] + LDS_K_BYTES;
-      Chunk<HD> ch;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int t = 8 * (r >> 2) + 4 * u + (r & 3);
-#pragma unroll
-        for (int kk = 0; kk < HD / 32; ++kk)
-          ch.k[u][kk] = *reinterpret_cast<const bf16x8*>(kimg + t * 256 + (((kk * 4 + h) ^ k_swz(t)) << 4));
-      }
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt) {
-        const int d = dt * 16 + r;
-        ch.v[dt] = *reinterpret_cast<const bf16x8*>(vimg + d * 64 + ((h ^ ((d >> 2) & 3)) << 4));
-      }
-      if ((c + 1) * CHUNK <= first_pos) {  // every key visible to every row of this wave
-#pragma unroll
-        for (int gt = 0; gt < GT; ++gt)
-          compute_chunk<HD, Causal, false>(ch, bq[gt], c * CHUNK, w_end, Causal{my_pos}, scale_log2, m[gt],
-                                           l[gt], o[gt], lane);
-      } else {
-#pragma unroll
-        for (int gt = 0; gt < GT; ++gt)
-          compute_chunk<HD, Causal, true>(ch, bq[gt], c * CHUNK, w_end, Causal{my_pos}, scale_log2, m[gt],
-                                          l[gt], o[gt], lane);
-      }
-    }
-    if (c + 1 < nchunk) commit(buf ^ 1);
-    __syncthreads();
-  }
-  if (!row_ok) return;
-#pragma unroll
-  for (int gt = 0; gt < GT; ++gt) {
-    const int qh = kvh * G + blockIdx.z * GT + gt;
-    const float inv = l[gt] > 0.f ? 1.f / l[gt] : 0.f;
-    bf16_t* orow = out + (static_cast<size_t>(my_row) * n_q + qh) * HD;
-#pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt) {
-      u16x4 v;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = f2bf(o[gt][dt][i] * inv);
-      *reinterpret_cast<u16x4*>(orow + dt * 16 + 4 * h) = v;
-    }
-  }
-}
-
-// ---- prefill, K/V staged global -> LDS by DMA (glds), 3-chunk ring ------------------
-// The register-direct kernel above is fed L2 -> CU: every wave loads its own K/V (16 KB
-// per 32-token chunk for 64 MFMAs at NT = 4; NT = 2 with twice the bytes per MFMA is
-// slower, so the feed is the limit).  Here a workgroup = 4 waves x 16 query rows x GT
-// heads of ONE kv head, and each K/V byte crosses L2 -> CU once per workgroup: a chunk
-// (8 KB K + 8 KB V) is 16 global_load_lds of 1 KB (waves 0-1: K rows, waves 2-3: V dims),
-// no staging registers, issued two chunks ahead into a ring of three 16-KB slots.
-// Per chunk c:  vmcnt(chunks issued after c) -> s_barrier -> glds of chunk c + 2 into the
-// slot chunk c - 1 used -> ds_read fragments of chunk c -> MFMAs.  RAW: a slot is read
-// after its issuing threads' counted vmcnt and a barrier; WAR: it is refilled only after
-// the barrier every wave passes once its reads of the previous use have been consumed.
-// Same swizzled images as the register-staged kernel (rows of K: 16 x 16-B pieces,
-// piece j at j ^ k_swz(t); rows of V^T: 4 pieces, piece hh at hh ^ ((d >> 2) & 3)): glds
-// writes lane l's 16 B at slot l, so the swizzle is applied to each lane's SOURCE piece.
-#ifndef DMA_RING
-#define DMA_RING 3  // 16-KB chunk slots (LEAD = DMA_RING - 1 chunks loaded ahead; 5 measured the same)
-#endif
-#ifndef DMA_LAZY
-#define DMA_LAZY false  // eager rescale: the lazy branch per head spills at GT = 5
-#endif
-constexpr int DMA_CHUNK_BYTES = LDS_K_BYTES + LDS_V_BYTES;  // 16 KiB
-
-template <int GT>
-__global__ __launch_bounds__(256, 1) void prefill_attn_dma_kernel(
-    const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
-    const int* __restrict__ q_start, const int* __restrict__ seq_lens, const int* __restrict__ tiles,
-    int n_q, float scale_log2, bf16_t* __restrict__ out) {
-  constexpr int HD = 128;
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[DMA_RING * DMA_CHUNK_BYTES];
-  const int tile = blockIdx.x, kvh = blockIdx.y;
-  const int G = n_q / g.n_kv;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r = lane & 15, h = lane >> 4;
-  const int b = tiles[3 * tile], q_begin = tiles[3 * tile + 1], q_end = tiles[3 * tile + 2];
-  const int ctx = seq_lens[b];
-  const int qs = q_start[b], qlen = q_start[b + 1] - qs;
-  const int pos0 = ctx - qlen;
-  const int* table = block_tables + static_cast<size_t>(b) * max_blocks;
-  const int kv_end = pos0 + (q_end - 1 - qs) + 1;  // keys visible to the tile's last row
-  const int nchunk = (kv_end + CHUNK - 1) / CHUNK;
-  const int nblk = (kv_end + BS - 1) / BS;
-
-  const int row0 = q_begin + 16 * w;
-  const bool wave_rows = row0 < q_end;  // wave-uniform; idle waves still stage K/V and hit barriers
-  const int my_row = row0 + r;
-  const bool row_ok = my_row < q_end;
-  const int my_pos = pos0 + (my_row - qs);
-  const int first_pos = pos0 + (row0 - qs);
-  const int w_end = wave_rows ? pos0 + (min(row0 + 15, q_end - 1) - qs) + 1 : 0;
-  bf16x8 bq[GT][HD / 32];
-  float m[GT], l[GT];
-  f32x4 o[GT][HD / 16];
-  // GT need not divide G: the heads past G of the last z-group are computed on a clamped
-  // head and never stored
-#pragma unroll
-  for (int gt = 0; gt < GT; ++gt) {
-    const int qh = kvh * G + min(static_cast<int>(blockIdx.z) * GT + gt, G - 1);
-    load_q<HD>(bq[gt], q + (static_cast<size_t>(row_ok ? my_row : (wave_rows ? row0 : q_begin)) * n_q + qh) * HD,
-               row_ok, lane);
-    m[gt] = -INFINITY;
-    l[gt] = 0.f;
-#pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt) o[gt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Q landed: from here vmcnt counts glds only
-
-  // this lane's source piece of glds i (0..3) of a chunk: waves 0-1 K rows, waves 2-3 V dims
-  auto issue = [&](int c) {
-    uint8_t* slot = smem + (c % DMA_RING) * DMA_CHUNK_BYTES;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const bf16_t* src;
-      uint8_t* dst;
-      if (w < 2) {
-        const int t = 16 * w + 4 * i + (lane >> 4);  // chunk token = K image row
-        const int j = (lane & 15) ^ k_swz(t);         // logical 16-B piece stored at slot (lane & 15)
-        const int blk = table[min(2 * c + (t >> 4), nblk - 1)];
-        src = g.k + block_base<HD>(g, blk, kvh) + (t & (BS - 1)) * HD + j * 8;
-        dst = slot + (16 * w + 4 * i) * 256;
-      } else {
-        const int d = 64 * (w - 2) + 16 * i + (lane >> 2);  // V^T image row
-        const int hh = (lane & 3) ^ ((d >> 2) & 3);
-        const int blk = table[min(2 * c + (hh >> 1), nblk - 1)];
-        src = g.v + block_base<HD>(g, blk, kvh) + d * BS + (hh & 1) * 8;
-        dst = slot + LDS_K_BYTES + (64 * (w - 2) + 16 * i) * 64;
-      }
-      __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
-    }
-  };
-
-  constexpr int LEAD = DMA_RING - 1;  // chunks in flight ahead of the one computed
-  static_assert(LEAD >= 1 && LEAD <= 4, "ring depth");
-#pragma unroll
-  for (int i = 0; i < LEAD; ++i)
-    if (i < nchunk) issue(i);
-  // one barrier per chunk for every wave: wait for chunk c, barrier, refill the freed slot
-  auto sync_issue = [&](int c) {
-    const int younger = min(LEAD - 1, nchunk - 1 - c);  // chunks issued after c, still allowed in flight
-    if (younger >= 3) {
-      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    } else if (younger == 2) {
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    } else if (younger == 1) {
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (c + LEAD < nchunk) issue(c + LEAD);  // into the slot of chunk c - 1: every wave is past its reads
-  };
-  auto read_chunk = [&](int c, Chunk<HD>& ch) {
-    const uint8_t* kimg = smem + (c % DMA_RING) * DMA_CHUNK_BYTES;
-    const uint8_t* vimg = kimg + LDS_K_BYTES;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int t = 8 * (r >> 2) + 4 * u + (r & 3);
-#pragma unroll
-      for (int kk = 0; kk < HD / 32; ++kk)
-        ch.k[u][kk] = *reinterpret_cast<const bf16x8*>(kimg + t * 256 + (((kk * 4 + h) ^ k_swz(t)) << 4));
-    }
-#pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt) {
-      const int d = dt * 16 + r;
-      ch.v[dt] = *reinterpret_cast<const bf16x8*>(vimg + d * 64 + ((h ^ ((d >> 2) & 3)) << 4));
-    }
-  };
-  // chunks every row of this wave sees in full: the GT heads as one straight-line block
-  // (full_scores / full_pv, as the NT sub-tiles of the register kernel), the lazy O rescale
-  // outside the inner loop; the wave's diagonal chunks and the rest of the tile afterwards
-  const int n_full = wave_rows ? min(first_pos / CHUNK, nchunk) : 0;
-  auto none = [](Chunk<HD>&) {};
-  int c = 0;
-  while (c < n_full) {
-    f32x4 sc[GT][2];
-    float mx[GT];
-    Chunk<HD> ch;
-    bool grow = false;
-    for (; c < n_full; ++c) {
-      sync_issue(c);
-      read_chunk(c, ch);
-      grow = full_scores<HD, GT, false>(ch, bq, scale_log2, m, sc, mx, none);
-      if (grow) break;  // wave-uniform
-      full_pv<HD, GT, false>(ch, sc, scale_log2, m, l, o, none);
-    }
-    if (!grow) break;
-    full_rescale<HD, GT>(mx, m, l, o);
-    full_pv<HD, GT, false>(ch, sc, scale_log2, m, l, o, none);
-    ++c;
-  }
-  for (; c < nchunk; ++c) {
-    sync_issue(c);
-    if (wave_rows && c * CHUNK < w_end) {  // wave-uniform
-      Chunk<HD> ch;
-      read_chunk(c, ch);
-#pragma unroll
-      for (int gt = 0; gt < GT; ++gt)
-        compute_chunk<HD, Causal, true, false, DMA_LAZY>(ch, bq[gt], c * CHUNK, w_end, Causal{my_pos}, scale_log2,
-                                                         m[gt], l[gt], o[gt], lane);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  if (!row_ok) return;
-#pragma unroll
-  for (int gt = 0; gt < GT; ++gt) {
-    if (static_cast<int>(blockIdx.z) * GT + gt >= G) break;
-    const int qh = kvh * G + blockIdx.z * GT + gt;
-    const float inv = l[gt] > 0.f ? 1.f / l[gt] : 0.f;
-    bf16_t* orow = out + (static_cast<size_t>(my_row) * n_q + qh) * HD;
-#pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt) {
-      u16x4 v;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = f2bf(o[gt][dt][i] * inv);
-      *reinterpret_cast<u16x4*>(orow + dt * 16 + 4 * h) = v;
-    }
-  }
-}
-
-// heads per workgroup for the LDS kernel: the largest divisor of G that is <= 5
-inline int lds_group_tile(int G) {
-  for (int gt = 5; gt >= 1; --gt)
-    if (G % gt == 0) return gt;
-  return 1;
-}
-
-int launch_prefill_lds(int n_tiles, int n_q, int n_kv, const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
-                       const int* q_start, const int* seq_lens, const int* tiles, float sl, bf16_t* out,
-                       hipStream_t stream, bool dma = false) {
-  const int G = n_q / n_kv;
-  int gt = lds_group_tile(G);
-  if (dma) {  // heads per workgroup of the glds kernel (BCG_PREFILL_GT, default min(G, 5))
-    static const int env_gt = [] {
-      const char* e = std::getenv("BCG_PREFILL_GT");
-      return e ? std::atoi(e) : 0;
-    }();
-    gt = env_gt >= 1 && env_gt <= 5 ? env_gt : std::min(G, 5);
-  }
-  const dim3 grid(n_tiles, n_kv, (G + gt - 1) / gt);
-  switch (gt) {
-#define BCG_LDS_CASE(GT)                                                                                         \
-  case GT:                                                                                                       \
-    if (dma)                                                                                                     \
-      hipLaunchKernelGGL(prefill_attn_dma_kernel<GT>, grid, dim3(256), 0, stream, q, g, tables, max_blocks,    \
-                         q_start, seq_lens, tiles, n_q, sl, out);                                                \
-    else                                                                                                         \
-      hipLaunchKernelGGL(prefill_attn_lds_kernel<GT>, grid, dim3(256), 0, stream, q, g, tables, max_blocks,    \
-                         q_start, seq_lens, tiles, n_q, sl, out);                                                \
-    break;
-    BCG_LDS_CASE(1)
-    BCG_LDS_CASE(2)
-    BCG_LDS_CASE(3)
-    BCG_LDS_CASE(4)
-    BCG_LDS_CASE(5)
-#undef BCG_LDS_CASE
-    default:
-      return -2;
-  }
-  return 0;
-}
-
 template <int HD, bool F8>
-int launch_prefill(int nt, int n_tiles, int n_q, const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
-                   const int* q_start, const int* seq_lens, const int* tiles, float sl, bf16_t* out,
-                   hipStream_t stream) {
-  switch (nt) {
-    case 1:
-      hipLaunchKernelGGL((prefill_attn_kernel<HD, 1, F8>), dim3(n_tiles, n_q), dim3(256), 0, stream, q, g, tables,
-                         max_blocks, q_start, seq_lens, tiles, n_q, sl, out);
-      break;
-    case 2:
-      hipLaunchKernelGGL((prefill_attn_kernel<HD, 2, F8>), dim3(n_tiles, (n_q + 1) / 2), dim3(256), 0, stream, q,
-                         g, tables, max_blocks, q_start, seq_lens, tiles, n_q, sl, out);
-      break;
-    case 4:
-      hipLaunchKernelGGL((prefill_attn_kernel<HD, 4, F8>), dim3(n_tiles, (n_q + 3) / 4), dim3(256), 0, stream, q,
-                         g, tables, max_blocks, q_start, seq_lens, tiles, n_q, sl, out);
-      break;
-    default:
-      return -2;
-  }
-  return 0;
+void launch_prefill(int n_tiles, int n_q, const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
+                    const int* q_start, const int* seq_lens, const int* tiles, float sl, bf16_t* out,
+                    hipStream_t stream) {
+  constexpr int NT = 4;  // 1 and 2 measured slower (PERF.md); the LDS-shared forms were 180-200 TF/s
+  hipLaunchKernelGGL((prefill_attn_kernel<HD, NT, F8>), dim3(n_tiles, (n_q + NT - 1) / NT), dim3(256), 0, stream, q,
+                     g, tables, max_blocks, q_start, seq_lens, tiles, n_q, sl, out);
 }
 
 }  // namespace
@@ -1108,16 +727,16 @@ BCG_API int bcg_paged_attention_decode(const void* q, const void* k_cache, const
   bf16_t* ob = static_cast<bf16_t*>(out);
   const float sl = scale * LOG2E;
   if (hd == 128 && kv_fp8) {
-    launch_decode<128, false, true, DEC_CPW>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace,
+    launch_decode<128, true, DEC_CPW>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace,
                                              max_splits, ob, stream);
   } else if (hd == 128) {
-    launch_decode<128, false, false, DEC_CPW>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace,
+    launch_decode<128, false, DEC_CPW>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace,
                                               max_splits, ob, stream);
   } else if (hd == 64 && kv_fp8) {
-    launch_decode<64, false, true, DEC_CPW>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace,
+    launch_decode<64, true, DEC_CPW>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace,
                                             max_splits, ob, stream);
   } else if (hd == 64) {
-    launch_decode<64, false, false, DEC_CPW>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace,
+    launch_decode<64, false, DEC_CPW>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace,
                                              max_splits, ob, stream);
   } else {
     return -2;
@@ -1125,31 +744,7 @@ BCG_API int bcg_paged_attention_decode(const void* q, const void* k_cache, const
   return BCG_CHECK_LAUNCH();
 }
 
-// Timing-only variants for tools/bench_ops.py (results are NOT valid attention
-// for the engine's cache layout): variant 1 = K read as [HD/32][BS][32] tiles.
-BCG_API int bcg_paged_attention_decode_exp(const void* q, const void* k_cache, const void* v_cache, int layer,
-                                           int num_blocks, int n_kv, const int* block_tables, int max_blocks,
-                                           const int* seq_lens, int B, int n_q, int hd, float scale,
-                                           float* workspace, int max_splits, int split_tokens, void* out,
-                                           int variant, hipStream_t stream) {
-  if (hd != 128 || n_q / n_kv > 16 || split_tokens != DEC_WAVES * CHUNK || B > DEC_MAX_B || max_splits > 64)
-    return -2;
-  KVGeom g{static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), layer, num_blocks, n_kv};
-  const float sl = scale * LOG2E;
-  if (variant == 2)  // two chunks per wave, both loaded up front (256-token items)
-    launch_decode<128, false, false, 2>(static_cast<const bf16_t*>(q), g, block_tables, max_blocks, seq_lens, B,
-                                        n_q, sl, workspace, max_splits, static_cast<bf16_t*>(out), stream);
-  else if (variant == 1)
-    launch_decode<128, true>(static_cast<const bf16_t*>(q), g, block_tables, max_blocks, seq_lens, B, n_q, sl,
-                             workspace, max_splits, static_cast<bf16_t*>(out), stream);
-  else
-    launch_decode<128, false>(static_cast<const bf16_t*>(q), g, block_tables, max_blocks, seq_lens, B, n_q, sl,
-                              workspace, max_splits, static_cast<bf16_t*>(out), stream);
-  return BCG_CHECK_LAUNCH();
-}
-
-// nt: query tiles of 16 rows per wave (1, 2 or 4) -- see prefill_attn_kernel; 0 = the LDS-shared
-// K/V kernel (bf16 caches, head_dim 128; other shapes fall back to nt = 4).
+// nt: 16-row query tiles per wave; only 4 is built (0 = default).
 BCG_API int bcg_paged_attention_prefill(const void* q, const void* k_cache, const void* v_cache, int layer,
                                         int num_blocks, int n_kv, const int* block_tables, int max_blocks,
                                         const int* q_start, const int* seq_lens, const int* tiles, int n_tiles,
@@ -1160,22 +755,18 @@ BCG_API int bcg_paged_attention_prefill(const void* q, const void* k_cache, cons
   const float sl = scale * LOG2E;
   const bf16_t* qb = static_cast<const bf16_t*>(q);
   bf16_t* ob = static_cast<bf16_t*>(out);
-  int rc;
-  if ((nt == 0 || nt == 8) && !(hd == 128 && !kv_fp8)) nt = 4;
-  if (nt == 0 || nt == 8)  // LDS-shared K/V: 0 = register-staged, 8 = glds ring
-    rc = launch_prefill_lds(n_tiles, n_q, n_kv, qb, g, block_tables, max_blocks, q_start, seq_lens, tiles, sl, ob,
-                            stream, nt == 8);
-  else if (hd == 128)
-    rc = kv_fp8 ? launch_prefill<128, true>(nt, n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens,
-                                            tiles, sl, ob, stream)
-                : launch_prefill<128, false>(nt, n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens,
-                                             tiles, sl, ob, stream);
+  if (nt != 0 && nt != 4) return -2;
+  if (hd == 128)
+    kv_fp8 ? launch_prefill<128, true>(n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens, tiles, sl,
+                                       ob, stream)
+           : launch_prefill<128, false>(n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens, tiles, sl,
+                                        ob, stream);
   else if (hd == 64)
-    rc = kv_fp8 ? launch_prefill<64, true>(nt, n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens,
-                                           tiles, sl, ob, stream)
-                : launch_prefill<64, false>(nt, n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens,
-                                            tiles, sl, ob, stream);
+    kv_fp8 ? launch_prefill<64, true>(n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens, tiles, sl,
+                                      ob, stream)
+           : launch_prefill<64, false>(n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens, tiles, sl,
+                                       ob, stream);
   else
     return -2;
-  return rc ? rc : BCG_CHECK_LAUNCH();
+  return BCG_CHECK_LAUNCH();
 }

@@ -3,7 +3,7 @@
   python tools/bench_ops.py [--model qwen3-14b] [--ms 16,40,80,128,160,192]
 
 Reports per-op time and effective HBM bandwidth (weight / KV bytes moved) for:
-  * decode projections: MFMA skinny GEMM vs torch.nn.functional.linear (hipBLASLt);
+  * decode projections: the GEMM plan (hand kernel / library) vs torch.nn.functional.linear (hipBLASLt);
   * paged decode attention (bytes = K+V of every context token);
   * the fused guided sampler.
 Writes a JSON summary to gpurun_out/bench_ops.json.
@@ -58,11 +58,11 @@ def main():
     for M in ([] if args.skip_gemm else [int(m) for m in args.ms.split(",")]):
         x = {k: torch.randn(M, kk, device="cuda", dtype=torch.bfloat16) for k, (n, kk) in shapes.items()}
         for name, w in weights.items():
-            t_sk = timeit(lambda: hip.linear(x[name], w)) if os.environ.get("BCG_SKINNY_GEMM") == "1" else 0.0
+            t_pl = timeit(lambda: hip.linear(x[name], w))
             t_bl = timeit(lambda: torch.nn.functional.linear(x[name], w))
             gb = w.numel() * 2 / 1e9
-            rec = {"M": M, "op": name, "skinny_us": round(t_sk, 1), "hipblaslt_us": round(t_bl, 1),
-                   "skinny_TBps": round(gb / t_sk * 1e3, 2) if t_sk else None, "hipblaslt_TBps": round(gb / t_bl * 1e3, 2)}
+            rec = {"M": M, "op": name, "plan_us": round(t_pl, 1), "hipblaslt_us": round(t_bl, 1),
+                   "plan_TBps": round(gb / t_pl * 1e3, 2), "hipblaslt_TBps": round(gb / t_bl * 1e3, 2)}
             out["gemm"].append(rec)
             print(json.dumps(rec), flush=True)
     # decode attention at the bench geometry
@@ -80,9 +80,6 @@ def main():
         t = timeit(lambda: hip.paged_attention_decode(q, k, v, 0, tables, seq, hd ** -0.5))
         gb = B * args.ctx * cfg.num_kv_heads * hd * 2 * 2 / 1e9
         rec = {"B": B, "ctx": args.ctx, "us": round(t, 1), "TBps": round(gb / t * 1e3, 2)}
-        for variant in [int(x) for x in os.environ.get("BCG_ATTN_VARIANTS", "").split(",") if x]:
-            tv = timeit(lambda: hip.paged_attention_decode_exp(q, k, v, 0, tables, seq, hd ** -0.5, variant))
-            rec[f"v{variant}_TBps"] = round(gb / tv * 1e3, 2)
         out["attention"].append(rec)
         print(json.dumps(rec), flush=True)
     # fused QK-norm + RoPE + paged KV write (decode rows and a prefill chunk)

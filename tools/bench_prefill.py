@@ -52,7 +52,7 @@ def gemms(cfg, M, mode):
     return res
 
 
-def attention(cfg, n_prompts, prompt, prefix, nt=None):
+def attention(cfg, n_prompts, prompt, prefix):
     from byzantine_consensus_llm_agents_amd.ops import get_ops
     hip = get_ops("hip")
     bs, hd = 16, cfg.head_dim
@@ -73,12 +73,12 @@ def attention(cfg, n_prompts, prompt, prefix, nt=None):
     q = torch.randn(T, n_q, hd, device="cuda", dtype=torch.bfloat16)
     seq_lens = torch.full((n_prompts,), ctx, dtype=torch.int32, device="cuda")
     us = timeit(lambda: hip.paged_attention_prefill(q, k, v, 0, tables, q_start.cuda(), seq_lens, hd ** -0.5,
-                                                    prompt, tiles, nt=nt))
+                                                    prompt, tiles))
     # causal FLOPs: each query sees prefix + its causal part
     flops = 4 * n_q * hd * n_prompts * (prompt * prefix + prompt * (prompt + 1) / 2)
-    r = {"prompts": n_prompts, "prompt": prompt, "prefix": prefix, "nt": nt, "us": round(us, 1),
+    r = {"prompts": n_prompts, "prompt": prompt, "prefix": prefix, "us": round(us, 1),
          "tflops": round(flops / us / 1e6, 1)}
-    print(f"[attn nt={nt}] {n_prompts}x{prompt} (+{prefix} cached) {us:9.1f} us {r['tflops']:7.1f} TF/s", flush=True)
+    print(f"[attn] {n_prompts}x{prompt} (+{prefix} cached) {us:9.1f} us {r['tflops']:7.1f} TF/s", flush=True)
     return r
 
 
@@ -90,7 +90,6 @@ def main():
     ap.add_argument("--skip-gemm", action="store_true")
     ap.add_argument("--skip-attn", action="store_true")
     ap.add_argument("--attn-model", default=None, help="model geometry for the attention runs")
-    ap.add_argument("--nts", default="0,4", help="prefill kernel forms to time (0 = LDS-staged, 1/2/4 = NT)")
     args = ap.parse_args()
     cfg = get_model_config(args.model)
     out = {"model": cfg.name, "gemm": {}, "attention": []}
@@ -112,9 +111,8 @@ def main():
         torch.backends.cuda.preferred_blas_library("cublaslt")
         torch.cuda.tunable.enable(False)
     acfg = get_model_config(args.attn_model) if args.attn_model else cfg
-    for nt in (() if args.skip_attn else [int(x) for x in args.nts.split(",")]):
-        for n, p, pre in ((12, 1024, 512), (16, 900, 400), (8, 2048, 0)):
-            out["attention"].append(attention(acfg, n, p, pre, nt))
+    for n, p, pre in (() if args.skip_attn else ((12, 1024, 512), (16, 900, 400), (8, 2048, 0))):
+        out["attention"].append(attention(acfg, n, p, pre))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "bench_prefill.json"), "w") as fh:
         json.dump(out, fh, indent=1)

@@ -11,7 +11,7 @@ while read -r group; do
   [ -z "$group" ] && continue
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $group --output-format csv -d $OUT/p$i -o run -- \
-    python tools/bench_prefill.py --skip-gemm --nts ${NTS:-0,4} > $OUT/p$i.log 2>&1
+    python tools/bench_prefill.py --skip-gemm > $OUT/p$i.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then echo "pass $i failed rc=$rc: $group"; grep -i -m3 "error" $OUT/p$i.log; exit 1; fi
   echo "pass $i ok: $group"
