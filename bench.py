@@ -66,11 +66,15 @@ def parse(argv=None):
                     help="decode batch cap (rows); default ENGINE_CONFIG['max_batch_seqs']")
     ap.add_argument("--ramp-s", type=float, default=None,
                     help="start the games spread over this many seconds (default: half the warmup)")
-    ap.add_argument("--age-p", type=float, default=0.2,
+    ap.add_argument("--age-p", type=float, default=0.15,
                     help="age-diverse pool: each slot's first game is burned in for A ~ Geometric(p) rounds "
                          "(scripted CPU engine, before any timed window); 0 = every game starts fresh")
-    ap.add_argument("--burnin-chars", default="400,200",
-                    help="internal_strategy,public_reasoning characters of the burn-in outputs")
+    ap.add_argument("--burnin-chars", default="320,420",
+                    help="internal_strategy,public_reasoning characters of the burn-in outputs "
+                         "(measured means of the engine's outputs: detail.age_mix.output_chars)")
+    ap.add_argument("--fill-max-s", type=float, default=240.0,
+                    help="before the warmup windows, wait (at most this long) until every game has "
+                         "finished its first decide phase: the start-up prefill wave is over")
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--max-rounds", type=int, default=50)
     ap.add_argument("--seed", type=int, default=1234)
@@ -84,6 +88,11 @@ def parse(argv=None):
                     help="prefill on a second HIP stream, concurrent with decode bursts (TP=1)")
     ap.add_argument("--no-custom-allreduce", action="store_true",
                     help="TP collectives through RCCL only (no xGMI one-/two-shot kernels)")
+    ap.add_argument("--kv-cache-gb", type=float, default=None,
+                    help="KV cache size per engine (default: from free memory x gpu_memory_utilization)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank on cuda:0, gloo process group, the xGMI "
+                         "all-reduce kernels forced over IPC peer buffers (never for measurements)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
 
@@ -161,6 +170,11 @@ class SimPool:
             for k in sim.counters:
                 sim.counters[k] = 0
             self.ages[i] = a
+
+    def filled(self) -> bool:
+        """Every slot's current game has completed at least one decide phase."""
+        with self.lock:
+            return all(s.counters["decisions_accepted"] > 0 or g > 0 for s, g in zip(self.sims, self.generation))
 
     def output_chars(self):
         """Mean public_reasoning / internal_strategy characters of the agents' latest outputs."""
@@ -263,14 +277,18 @@ def main(argv=None):
 
     gpu = args.backend == "hip"
     ctrl = None
+    if args.one_device:
+        local = 0
+        os.environ["BCG_CUSTOM_AR"] = "force"
     if gpu:
         torch.cuda.set_device(local)
     if world > 1:
         import datetime
-        dist.init_process_group("nccl" if gpu else "gloo", timeout=datetime.timedelta(seconds=900))
+        dist.init_process_group("nccl" if gpu and not args.one_device else "gloo",
+                                timeout=datetime.timedelta(seconds=900))
         # control plane (barriers, result reduction) on a CPU group: never queued on a
         # HIP stream behind the engine's kernels / TP collectives
-        ctrl = dist.new_group(backend="gloo") if gpu else dist.group.WORLD
+        ctrl = dist.new_group(backend="gloo") if gpu and not args.one_device else dist.group.WORLD
 
     from byzantine_consensus_llm_agents_amd.bcg import config as C
     from byzantine_consensus_llm_agents_amd.bcg.engine_agent import EngineAgent
@@ -289,6 +307,8 @@ def main(argv=None):
                            kv_cache_dtype=args.kv_cache_dtype)
     if args.max_batch_seqs:
         C.ENGINE_CONFIG["max_batch_seqs"] = args.max_batch_seqs
+    if args.kv_cache_gb:
+        C.ENGINE_CONFIG["kv_cache_gb"] = args.kv_cache_gb
     C.BCG_CONFIG["value_range"] = (0, 50)
     random.seed(args.seed + rank)
 
@@ -334,9 +354,21 @@ def main(argv=None):
         pool.check()
         return pool.accepted()
 
+    # Pool fill (untimed, before the warmup windows): all games start within the ramp, so their
+    # first prompts arrive as one prefill wave that a long-running pool never sees; wait until
+    # every game has finished its first decide phase.  TP followers / other DP ranks wait at the
+    # barrier below.
+    t_fill = time.perf_counter()
+    if pool is not None:
+        deadline_fill = t_fill + args.fill_max_s
+        while time.perf_counter() < deadline_fill and not pool.filled():
+            pool.check()
+            time.sleep(0.5)
+    fill_s = time.perf_counter() - t_fill
+    barrier()
     time.sleep(args.window_s * args.warmup)
     if rank == 0:
-        print(f"[warmup] {args.warmup} x {args.window_s}s windows, accepted={accepted()} "
+        print(f"[warmup] fill {fill_s:.1f}s + {args.warmup} x {args.window_s}s windows, accepted={accepted()} "
               f"init={init_s:.1f}s", file=sys.stderr, flush=True)
 
     eng = getattr(llm.backend, "stats", {})
@@ -407,6 +439,7 @@ def main(argv=None):
                        "decisions_per_window_rank0": per_window,
                        "first5_vs_last5": [round(sum(per_window[:5]) / max(1, len(per_window[:5])), 1),
                                            round(sum(per_window[-5:]) / max(1, len(per_window[-5:])), 1)],
+                       "fill_s": round(fill_s, 1),
                        "age_mix": {"p": args.age_p, "burnin_chars": args.burnin_chars,
                                    "mean_burnin_rounds": (round(sum(pool.ages) / len(pool.ages), 2)
                                                           if pool else None),

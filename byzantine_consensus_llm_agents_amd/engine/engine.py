@@ -457,12 +457,14 @@ class InferenceEngine:
     # ---- TP plan exchange (driver -> followers, CPU group) ----
     def _send_plan(self, plan: dict):
         import torch.distributed as dist
-        dist.broadcast_object_list([plan], src=self.tp.leader, group=self.tp.ctrl)
+        with self.timer.phase("plan_exchange"):
+            dist.broadcast_object_list([plan], src=self.tp.leader, group=self.tp.ctrl)
 
     def _recv_plan(self) -> dict:
         import torch.distributed as dist
         box = [None]
-        dist.broadcast_object_list(box, src=self.tp.leader, group=self.tp.ctrl)
+        with self.timer.phase("plan_wait"):  # follower: includes waiting for the driver's next iteration
+            dist.broadcast_object_list(box, src=self.tp.leader, group=self.tp.ctrl)
         return box[0]
 
     @staticmethod

@@ -7,10 +7,11 @@ One forward serves both phases:
 * decode  - one token per sequence (``T = B``), captured into a HIP graph by
   the engine.
 
-Per layer: fused residual-add+RMSNorm -> QKV GEMM (hipBLASLt)
--> fused QK-norm+RoPE+paged-KV-write (HIP) -> paged attention (HIP, MFMA) ->
-o_proj GEMM [-> RCCL all-reduce] -> fused add+RMSNorm -> gate_up GEMM ->
-SiLU*mul (HIP) -> down GEMM [-> RCCL all-reduce].  Column-parallel
+Per layer: fused residual-add+RMSNorm -> QKV GEMM -> fused
+QK-norm+RoPE+paged-KV-write (HIP) -> paged attention (HIP, MFMA) -> o_proj GEMM
+[-> all-reduce fused with the next add+RMSNorm] -> gate_up GEMM with SiLU*mul in its
+epilogue -> down GEMM [-> all-reduce fused with the next add+RMSNorm]; at TP=1 the
+residual adds ride in the o/down GEMM epilogues.  Column-parallel
 QKV/gate_up, row-parallel o/down, vocab-parallel LM head + all-gather, so a
 TP group does 2L+1 collectives per forward like the reference's vLLM path.
 """
@@ -278,50 +279,83 @@ class DecoderModel:
         """Returns logits ``[len(logits_idx) or B, vocab]`` (full vocab, fp32 or bf16)."""
         if self.quant is None and self.tp.size == 1 and hasattr(self.ops, "linear_residual"):
             return self._forward_fused(tokens, meta, k_cache, v_cache)
+        return self._forward_general(tokens, meta, k_cache, v_cache)
+
+    def _attention(self, li, L, qkv, meta, k_cache, v_cache):
         ops, c = self.ops, self.cfg
-        fp8 = self.quant == "fp8"
-        residual = None
-        x = F.embedding(tokens.long(), self.embed) if fp8 else None
+        q = ops.qk_norm_rope_kv_write(qkv, meta.positions, meta.slots, self.n_q, self.n_kv, self.hd,
+                                      L.get("q_norm"), L.get("k_norm"), c.rms_eps, self.cos_sin,
+                                      k_cache, v_cache, li)
+        if meta.decode:
+            return ops.paged_attention_decode(q, k_cache, v_cache, li, meta.block_tables, meta.seq_lens,
+                                              self.scale, meta.workspace)
+        return ops.paged_attention_prefill(q, k_cache, v_cache, li, meta.block_tables, meta.q_start,
+                                           meta.seq_lens, self.scale, meta.max_q_len, meta.tiles)
+
+    def _forward_general(self, tokens, meta, k_cache, v_cache):
+        """Tensor-parallel and / or fp8 forward, with the same fusions as the TP=1 bf16 path
+        where the math allows them:
+
+        * first layer: embedding gather + RMSNorm (+ fp8 quant) in one kernel;
+        * TP (row-parallel o / down): the rank's partial output goes straight into the fused
+          all-reduce + residual add + RMSNorm (xGMI kernel, RCCL + add_rmsnorm beyond it);
+          under fp8 the row-wise quant follows on the normed rows;
+        * TP=1 fp8: o / down add into the residual stream in the fp8 GEMM epilogue, then a
+          plain RMSNorm + quant (no separate residual pass);
+        * bf16 gate_up: SiLU * up fused into the GEMM epilogue (``linear_silu``) -- the
+          column-parallel shard [gate_r; up_r] is local, so this holds under TP too;
+        * fp8 gate_up: SiLU * up fused with the quant of the down projection's input;
+        * the final norm and LM head run on the logits rows only (selected BEFORE the last
+          all-reduce: the reduction is row-wise).
+        """
+        ops, c, tp = self.ops, self.cfg, self.tp
+        fp8, tp1 = self.quant == "fp8", self.tp.size == 1
+        eps = c.rms_eps
+        residual = x = h = hq = hs = None
         for li, L in enumerate(self.layers):
-            if fp8:  # norm + row-wise fp8 quant fused; hipBLASLt fp8 GEMM
-                hq, hs, residual = ops.add_rmsnorm_fp8(x, residual, L["ln1"], c.rms_eps)
-                qkv = ops.linear_fp8(hq, hs, L["qkv"], L["qkv_s"], L.get("qkv_bias"))
+            # ---- input norm (the previous layer's down projection is reduced here) ----
+            if li == 0:
+                if fp8:
+                    hq, hs, residual = ops.embed_rmsnorm_fp8(tokens, self.embed, L["ln1"], eps)
+                else:
+                    h, residual = ops.embed_rmsnorm(tokens, self.embed, L["ln1"], eps)
+            elif fp8 and tp1:
+                hq, hs = ops.rmsnorm_fp8(residual, L["ln1"], eps)
             else:
-                if li == 0:  # embedding gather fused with the first input norm
-                    h, residual = ops.embed_rmsnorm(tokens, self.embed, L["ln1"], c.rms_eps)
-                else:  # x: this rank's partial down_proj output of the previous layer
-                    h, residual = self.tp.all_reduce_add_rmsnorm(x, residual, L["ln1"], c.rms_eps, ops)
-                qkv = ops.linear(h, L["qkv"], L.get("qkv_bias"))
-            q = ops.qk_norm_rope_kv_write(qkv, meta.positions, meta.slots, self.n_q, self.n_kv, self.hd,
-                                          L.get("q_norm"), L.get("k_norm"), c.rms_eps, self.cos_sin,
-                                          k_cache, v_cache, li)
-            if meta.decode:
-                attn = ops.paged_attention_decode(q, k_cache, v_cache, li, meta.block_tables,
-                                                  meta.seq_lens, self.scale, meta.workspace)
-            else:
-                attn = ops.paged_attention_prefill(q, k_cache, v_cache, li, meta.block_tables,
-                                                   meta.q_start, meta.seq_lens, self.scale, meta.max_q_len,
-                                                   meta.tiles)
+                h, residual = tp.all_reduce_add_rmsnorm(x, residual, L["ln1"], eps, ops)
+                if fp8:
+                    hq, hs = ops.quant_fp8(h)
+            qkv = (ops.linear_fp8(hq, hs, L["qkv"], L["qkv_s"], L.get("qkv_bias")) if fp8
+                   else ops.linear(h, L["qkv"], L.get("qkv_bias")))
+            attn = self._attention(li, L, qkv, meta, k_cache, v_cache)
+            # ---- o_proj, post-attention norm, MLP ----
             if fp8:
                 aq, as_ = ops.quant_fp8(attn)
-                x = self.tp.all_reduce_(ops.linear_fp8(aq, as_, L["o"], L["o_s"]))
-                hq, hs, residual = ops.add_rmsnorm_fp8(x, residual, L["ln2"], c.rms_eps)
-                gu = ops.linear_fp8(hq, hs, L["gate_up"], L["gate_up_s"])
-                mq, ms = ops.silu_mul_fp8(gu)
-                x = self.tp.all_reduce_(ops.linear_fp8(mq, ms, L["down"], L["down_s"]))
+                if tp1:
+                    ops.linear_fp8_residual(aq, as_, L["o"], L["o_s"], residual)
+                    hq, hs = ops.rmsnorm_fp8(residual, L["ln2"], eps)
+                else:
+                    h, residual = tp.all_reduce_add_rmsnorm(ops.linear_fp8(aq, as_, L["o"], L["o_s"]), residual,
+                                                            L["ln2"], eps, ops)
+                    hq, hs = ops.quant_fp8(h)
+                mq, ms = ops.silu_mul_fp8(ops.linear_fp8(hq, hs, L["gate_up"], L["gate_up_s"]))
+                if tp1:
+                    ops.linear_fp8_residual(mq, ms, L["down"], L["down_s"], residual)
+                else:
+                    x = ops.linear_fp8(mq, ms, L["down"], L["down_s"])  # partial: reduced at the next norm
             else:
-                h, residual = self.tp.all_reduce_add_rmsnorm(ops.linear(attn, L["o"]), residual, L["ln2"],
-                                                             c.rms_eps, ops)
-                gu = ops.linear(h, L["gate_up"])
-                x = ops.linear(ops.silu_mul(gu), L["down"])  # partial: reduced at the next norm
-        if not fp8:
-            x = self.tp.all_reduce_(x)
+                h, residual = tp.all_reduce_add_rmsnorm(ops.linear(attn, L["o"]), residual, L["ln2"], eps, ops)
+                x = ops.linear(ops.linear_silu(h, L["gate_up"]), L["down"])  # partial: reduced at the next norm
         if meta.logits_idx is not None:
-            x = x.index_select(0, meta.logits_idx)
             residual = residual.index_select(0, meta.logits_idx)
-        h, _ = ops.add_rmsnorm(x, residual, self.final_norm, c.rms_eps)
+            if x is not None and not tp1:
+                x = x.index_select(0, meta.logits_idx)
+        if tp1 and fp8:
+            h = ops.rmsnorm(residual, self.final_norm, eps)
+        else:
+            h, _ = tp.all_reduce_add_rmsnorm(x, residual, self.final_norm, eps, ops)
         logits = ops.linear(h, self.lm_head)
-        return self.tp.all_gather_last(logits)
+        return tp.all_gather_last(logits)
 
     def _forward_fused(self, tokens, meta, k_cache, v_cache):
         """TP=1 bf16 forward with the GEMM epilogues fused (hand MFMA kernel where the
@@ -342,16 +376,7 @@ class DecoderModel:
             else:
                 h = ops.rmsnorm(residual, L["ln1"], c.rms_eps)
             qkv = ops.linear(h, L["qkv"], L.get("qkv_bias"))
-            q = ops.qk_norm_rope_kv_write(qkv, meta.positions, meta.slots, self.n_q, self.n_kv, self.hd,
-                                          L.get("q_norm"), L.get("k_norm"), c.rms_eps, self.cos_sin,
-                                          k_cache, v_cache, li)
-            if meta.decode:
-                attn = ops.paged_attention_decode(q, k_cache, v_cache, li, meta.block_tables,
-                                                  meta.seq_lens, self.scale, meta.workspace)
-            else:
-                attn = ops.paged_attention_prefill(q, k_cache, v_cache, li, meta.block_tables,
-                                                   meta.q_start, meta.seq_lens, self.scale, meta.max_q_len,
-                                                   meta.tiles)
+            attn = self._attention(li, L, qkv, meta, k_cache, v_cache)
             residual = ops.linear_residual(attn, L["o"], residual)
             h = ops.rmsnorm(residual, L["ln2"], c.rms_eps)
             act = ops.linear_silu(h, L["gate_up"])

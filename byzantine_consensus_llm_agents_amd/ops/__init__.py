@@ -38,6 +38,9 @@ def _torch_ops() -> SimpleNamespace:
         add_rmsnorm_fp8=_ref.add_rmsnorm_fp8,
         silu_mul_fp8=_ref.silu_mul_fp8,
         linear_fp8=_ref.linear_fp8,
+        rmsnorm_fp8=_ref.rmsnorm_fp8,
+        embed_rmsnorm_fp8=_ref.embed_rmsnorm_fp8,
+        linear_fp8_residual=_ref.linear_fp8_residual,
     )
 
 

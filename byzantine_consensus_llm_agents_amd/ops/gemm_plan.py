@@ -30,8 +30,10 @@ from typing import Dict, Optional, Tuple
 TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "engine", "tuned",
                      "hand_gemm.json")
 TILES = ((128, 128), (64, 128), (128, 64), (256, 128), (64, 256), (64, 64), (32, 128),  # csrc/kernels/gemm.hip CFGS
-         (256, 128), (128, 256), (128, 128), (256, 256))
+         (256, 128), (128, 256), (128, 128), (256, 256), (256, 256))
 PP_CFG = 10  # csrc/kernels/gemm_pp.hip: 256 x 256 ping-pong tile, N only a multiple of 16
+RS_CFG = 11  # csrc/kernels/gemm_rs.hip: 256 x 256 register-staged tile, same shape rules
+BIG_CFGS = (PP_CFG, RS_CFG)
 N_CFGS = len(TILES)
 SPLITS = (1, 2, 3, 4, 6, 8)
 
@@ -64,8 +66,8 @@ class GemmPlan:
         if cfg not in self.tiles or M <= 0 or K % 64 or K <= 0 or split_k < 1 or K // 64 < split_k:
             return False
         bn = self.tiles[cfg][1]
-        if cfg == PP_CFG:  # 32-bit buffer offsets: operands below 4 GiB
-            return (N % 16 == 0 and 2 * M * K < 1 << 32 and 2 * N * K < 1 << 32
+        if cfg in BIG_CFGS:  # 32-bit buffer offsets: operands below 4 GiB
+            return (N % 16 == 0 and 2 * (M + 256) * K < 1 << 32 and 2 * (N + 256) * K < 1 << 32
                     and (epi != 1 or (N % 2 == 0 and (N // 2) % 128 == 0)))
         if N % bn:
             return False
@@ -144,6 +146,6 @@ class Fp8Plan:
             return None
         else:
             cfg, split = (6 if M <= 32 else 1 if M <= 64 else 0), 1
-        if cfg < 0 or cfg not in self.tiles or cfg == PP_CFG or N % self.tiles[cfg][1] or K // 128 < split:
+        if cfg < 0 or cfg not in self.tiles or cfg in BIG_CFGS or N % self.tiles[cfg][1] or K // 128 < split:
             return None
         return (cfg, split)

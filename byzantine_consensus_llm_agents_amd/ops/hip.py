@@ -47,6 +47,8 @@ def load_library(path: str = None) -> ctypes.CDLL:
         "bcg_add_rmsnorm_fp8": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_int,
                                 c_void_p],
         "bcg_silu_mul_fp8": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+        "bcg_embed_rmsnorm_fp8": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,
+                                  c_void_p],
         "bcg_gemm_nt": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_int, c_int, c_int, c_int, c_int, c_void_p],
         "bcg_gemm_nt_fp8": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -350,6 +352,29 @@ def hip_ops() -> SimpleNamespace:
                                        _stream()), "add_rmsnorm_fp8")
         return q, s, residual
 
+    def rmsnorm_fp8(x, w, eps):
+        """Plain RMSNorm + row-wise fp8 quant (the residual stream was updated by the GEMM epilogue)."""
+        _req(x.dtype == torch.bfloat16 and x.is_contiguous() and x.dim() == 2, "rmsnorm_fp8: x bf16 [T,H]")
+        T, H = x.shape
+        _req(w.shape == (H,) and w.dtype == torch.bfloat16, "rmsnorm_fp8: weight [H] bf16")
+        q = torch.empty(T, H, dtype=f8, device=x.device)
+        s = torch.empty(T, dtype=torch.float32, device=x.device)
+        _check(lib.bcg_add_rmsnorm_fp8(_p(x), None, _p(w), _p(q), _p(s), T, H, eps, 2, _stream()), "rmsnorm_fp8")
+        return q, s
+
+    def embed_rmsnorm_fp8(tokens, table, w, eps):
+        """(fp8(rmsnorm(table[tokens]) * w), row scales, table[tokens]) in one pass."""
+        _req(tokens.dtype == torch.int32 and tokens.is_contiguous() and tokens.dim() == 1, "tokens int32 [T]")
+        _req(table.dtype == torch.bfloat16 and table.is_contiguous() and table.dim() == 2, "table bf16 [V,H]")
+        T, H = tokens.numel(), table.shape[1]
+        _req(w.shape == (H,) and w.dtype == torch.bfloat16, "embed_rmsnorm_fp8: weight [H] bf16")
+        residual = torch.empty(T, H, dtype=table.dtype, device=table.device)
+        q = torch.empty(T, H, dtype=f8, device=table.device)
+        s = torch.empty(T, dtype=torch.float32, device=table.device)
+        _check(lib.bcg_embed_rmsnorm_fp8(_p(tokens), _p(table), _p(w), _p(residual), _p(q), _p(s), T, H, eps,
+                                         _stream()), "embed_rmsnorm_fp8")
+        return q, s, residual
+
     def silu_mul_fp8(gu):
         _req(gu.dtype == torch.bfloat16 and gu.is_contiguous() and gu.dim() == 2 and gu.shape[1] % 16 == 0,
              "silu_mul_fp8: bf16 [T,2I]")
@@ -408,7 +433,20 @@ def hip_ops() -> SimpleNamespace:
         return torch._scaled_mm(xq, wq.t(), scale_a=xs.view(-1, 1), scale_b=ws.view(1, -1), bias=bias,
                                 out_dtype=out_dtype)
 
-    return SimpleNamespace(name="hip", linear=linear, linear_silu=linear_silu, linear_residual=linear_residual,
+    def linear_fp8_residual(xq, xs, wq, ws, residual):
+        """residual <- residual + dequant(xq . wq^T) in place: the o/down projection's residual
+        update in the hand fp8 kernel's epilogue (hipBLASLt + a separate add otherwise)."""
+        _req(residual.dtype == torch.bfloat16 and residual.is_contiguous()
+             and residual.shape == (xq.shape[0], wq.shape[0]), "linear_fp8_residual: residual [M,N] bf16")
+        if xq.is_contiguous() and wq.is_contiguous():
+            cfg = fp8_cfg(xq.shape[0], wq.shape[0], xq.shape[1])
+            if cfg is not None:
+                return gemm_nt_fp8(xq, xs.contiguous(), wq, ws.contiguous(), cfg, 2, residual=residual,
+                                   out=residual)
+        return residual.add_(linear_fp8(xq, xs, wq, ws))
+
+    return SimpleNamespace(name="hip", rmsnorm_fp8=rmsnorm_fp8, embed_rmsnorm_fp8=embed_rmsnorm_fp8,
+                           linear_fp8_residual=linear_fp8_residual, linear=linear, linear_silu=linear_silu, linear_residual=linear_residual,
                            gemm_nt=gemm_nt, gemm_plan=plan, prepare_device=prepare_device,
                            register_stream=register_stream, quant_fp8=quant_fp8, add_rmsnorm_fp8=add_rmsnorm_fp8,
                            silu_mul_fp8=silu_mul_fp8, linear_fp8=linear_fp8, gemm_nt_fp8=gemm_nt_fp8, fp8_cfg=fp8_cfg, rmsnorm=rmsnorm, add_rmsnorm=add_rmsnorm, silu_mul=silu_mul,

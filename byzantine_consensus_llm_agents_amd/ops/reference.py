@@ -247,6 +247,25 @@ def add_rmsnorm_fp8(x, residual, w, eps):
     return q, s, residual
 
 
+def rmsnorm_fp8(x, w, eps):
+    """Plain RMSNorm (bf16-rounded, as the bf16 path) then row-wise fp8 quantisation."""
+    return quant_fp8(rmsnorm(x, w, eps))
+
+
+def embed_rmsnorm_fp8(tokens, table, w, eps):
+    """(fp8(rmsnorm(table[tokens]) * w), row scales, table[tokens])."""
+    y, residual = embed_rmsnorm(tokens, table, w, eps)
+    q, s = quant_fp8(y)
+    return q, s, residual
+
+
+def linear_fp8_residual(xq, xs, wq, ws, residual):
+    """residual <- residual + dequant(xq . wq^T), rounded once (the fused fp8 epilogue); in place."""
+    y = (xq.float() * xs[:, None]) @ (wq.float() * ws[:, None]).t()
+    residual.copy_((residual.float() + y).to(residual.dtype))
+    return residual
+
+
 def silu_mul_fp8(gu):
     return quant_fp8(silu_mul(gu))
 

@@ -1,4 +1,4 @@
-// Standalone timing harness for csrc/kernels/gemm_pp.hip (one variant per binary: build-time
+// Standalone timing harness for csrc/kernels/gemm_pp.hip / gemm_rs.hip (one variant per binary: build-time
 // -D switches, so variants do not perturb each other's codegen -- cdna_hip_programming.md
 // §5.4 rule 19).  Random bf16 operands (hash-based, |x| < 1), weights rotated over copies
 // that exceed the 256 MiB Infinity Cache, hipEvent timing of back-to-back launches.
@@ -10,8 +10,11 @@
 
 #include <vector>
 
-extern "C" int bcg_gemm_pp(int epi, const void* x, const void* w, const void* bias, const void* residual, void* c,
-                           void* ws, void* counters, int M, int N, int K, int inter, int split_k, hipStream_t stream);
+#ifndef GEMM_FN
+#define GEMM_FN bcg_gemm_pp  // or bcg_gemm_rs (csrc/kernels/gemm_rs.hip): same contract
+#endif
+extern "C" int GEMM_FN(int epi, const void* x, const void* w, const void* bias, const void* residual, void* c,
+                       void* ws, void* counters, int M, int N, int K, int inter, int split_k, hipStream_t stream);
 
 __global__ void fill_bf16(uint16_t* p, size_t n, uint32_t seed, float scale) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -66,7 +69,7 @@ int main(int argc, char** argv) {
   auto run = [&](int i) {
     const void* res = epi == 2 ? r : nullptr;
     void* out = epi == 2 ? (void*)r : (void*)c;
-    return bcg_gemm_pp(epi, x, w[i % copies], nullptr, res, out, ws, cnt, M, N, K, N / 2, split, 0);
+    return GEMM_FN(epi, x, w[i % copies], nullptr, res, out, ws, cnt, M, N, K, N / 2, split, 0);
   };
   for (int i = 0; i < 5; ++i)
     if (run(i)) {

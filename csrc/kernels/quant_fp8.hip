@@ -7,6 +7,8 @@
 // ~2x the bf16 rate.  The quantisation is fused into the producers so the fp8
 // path adds no extra pass over the activations:
 //   add_rmsnorm_fp8 : residual add + RMSNorm (bf16-rounded, as the bf16 path) + quant
+//                     (also: plain RMSNorm + quant after a residual GEMM epilogue, and the
+//                     embedding gather + RMSNorm + quant of the first layer)
 //   silu_mul_fp8    : SiLU(gate) * up (bf16-rounded) + quant
 //   quant_fp8       : stand-alone (attention output before o_proj)
 // One 256-thread workgroup per row; the row max is a wave64 shuffle reduction
@@ -69,13 +71,18 @@ __global__ __launch_bounds__(QT) void quant_fp8_kernel(const bf16_t* __restrict_
   }
 }
 
+// has_residual: 0 = residual <- x, 1 = residual <- residual + x, 2 = plain RMSNorm of x (the
+// residual stream was updated by the GEMM epilogue that produced x: nothing written back).
+// gather != nullptr: x row = table row gather[row] (the embedding lookup fused in).
 __global__ __launch_bounds__(QT) void add_rmsnorm_fp8_kernel(
     const bf16_t* __restrict__ x, bf16_t* __restrict__ residual, const bf16_t* __restrict__ w,
-    uint8_t* __restrict__ q, float* __restrict__ scale, int H, float eps, int has_residual) {
+    uint8_t* __restrict__ q, float* __restrict__ scale, int H, float eps, int has_residual,
+    const int* __restrict__ gather) {
   __shared__ float red[QT / WAVE];
   const int tid = threadIdx.x;
   const int nvec = H / 8;
   const size_t base = static_cast<size_t>(blockIdx.x) * H;
+  if (gather) x += static_cast<size_t>(gather[blockIdx.x]) * H - base;
   float v[NORM_MAX_CHUNK][8];
   float ss = 0.f;
 #pragma unroll
@@ -84,18 +91,18 @@ __global__ __launch_bounds__(QT) void add_rmsnorm_fp8_kernel(
     if (vi < nvec) {
       const u16x8 xv = *reinterpret_cast<const u16x8*>(x + base + vi * 8);
       u16x8 rv;
-      if (has_residual) rv = *reinterpret_cast<const u16x8*>(residual + base + vi * 8);
+      if (has_residual == 1) rv = *reinterpret_cast<const u16x8*>(residual + base + vi * 8);
       u16x8 nr;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float f = bf2f(xv[j]);
-        if (has_residual) f += bf2f(rv[j]);
+        if (has_residual == 1) f += bf2f(rv[j]);
         nr[j] = f2bf(f);
         f = bf2f(nr[j]);
         v[c][j] = f;
         ss += f * f;
       }
-      *reinterpret_cast<u16x8*>(residual + base + vi * 8) = nr;
+      if (has_residual != 2) *reinterpret_cast<u16x8*>(residual + base + vi * 8) = nr;
     }
   }
   ss = wave_sum(ss);
@@ -171,10 +178,21 @@ BCG_API int bcg_quant_fp8(const void* x, void* q, float* scale, int T, int K, hi
 
 BCG_API int bcg_add_rmsnorm_fp8(const void* x, void* residual, const void* w, void* q, float* scale, int T, int H,
                                 float eps, int has_residual, hipStream_t stream) {
-  if (H % 8 || H > QT * 8 * NORM_MAX_CHUNK || T <= 0) return -2;
+  if (H % 8 || H > QT * 8 * NORM_MAX_CHUNK || T <= 0 || has_residual < 0 || has_residual > 2) return -2;
   hipLaunchKernelGGL(add_rmsnorm_fp8_kernel, dim3(T), dim3(QT), 0, stream, static_cast<const bf16_t*>(x),
                      static_cast<bf16_t*>(residual), static_cast<const bf16_t*>(w), static_cast<uint8_t*>(q),
-                     scale, H, eps, has_residual);
+                     scale, H, eps, has_residual, static_cast<const int*>(nullptr));
+  return BCG_CHECK_LAUNCH();
+}
+
+// residual[t] <- table[tokens[t]]; (q, scale)[t] <- fp8(rmsnorm(residual[t]) * w): the fp8 path's
+// first layer input in one pass.  Token ids must be < vocab (checked by their producers).
+BCG_API int bcg_embed_rmsnorm_fp8(const int* tokens, const void* table, const void* w, void* residual, void* q,
+                                  float* scale, int T, int H, float eps, hipStream_t stream) {
+  if (H % 8 || H > QT * 8 * NORM_MAX_CHUNK || T <= 0) return -2;
+  hipLaunchKernelGGL(add_rmsnorm_fp8_kernel, dim3(T), dim3(QT), 0, stream, static_cast<const bf16_t*>(table),
+                     static_cast<bf16_t*>(residual), static_cast<const bf16_t*>(w), static_cast<uint8_t*>(q),
+                     scale, H, eps, 0, tokens);
   return BCG_CHECK_LAUNCH();
 }
 

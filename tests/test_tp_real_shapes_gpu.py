@@ -1,0 +1,125 @@
+"""Tensor parallelism at the REAL layer shapes of BASELINE configs 4 and 5, rehearsed on one GPU.
+
+* config 4: Qwen3-32B (H 5120, 64 q / 8 kv heads, I 25600, vocab 151936) at TP = 4;
+* config 5: Mistral-Small-22B (H 6144, 48 / 8 heads, I 16384, vocab 32768) with fp8
+  projections at TP = 2.
+
+The layer count is cut to 4 (every per-layer shape, shard split, GEMM table entry and
+collective message size is the real one; only the depth, i.e. the run time, is not).
+The TP ranks are processes sharing cuda:0 (gloo control group; the custom xGMI all-reduce
+kernels run over IPC-mapped peer buffers, ``BCG_CUSTOM_AR=force``), each holding its own
+shards of the SAME random weights as the TP = 1 model (``init_random`` draws every full
+tensor from its own seeded stream and slices it like a checkpoint).
+
+Checked, per config: a packed prefill of 8 prompts, then 24 teacher-forced decode steps
+(every run is fed the TP = 1 greedy tokens): the TP logits equal the TP = 1 logits to bf16
+tolerance, greedy picks agree, and every rank holds bitwise-identical logits.
+"""
+import dataclasses
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+N_LAYERS, STEPS, BS = 4, 24, 16
+LENS = [37, 150, 301, 64, 90, 411, 16, 222]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _cfg(name):
+    from byzantine_consensus_llm_agents_amd.models.config import get_model_config
+    return dataclasses.replace(get_model_config(name), num_layers=N_LAYERS)
+
+
+def _run(name, quant, tp, forced=None):
+    """Prefill + STEPS decode steps; returns (per-step logits [B, V] fp32 cpu, greedy tokens)."""
+    from byzantine_consensus_llm_agents_amd.models.transformer import AttnMeta, DecoderModel
+    from byzantine_consensus_llm_agents_amd.ops import get_ops
+    cfg = _cfg(name)
+    m = DecoderModel(cfg, get_ops("hip"), "cuda", torch.bfloat16, tp, quant=quant)
+    m.init_random(seed=7, std=0.02)
+    B = len(LENS)
+    nb = (max(LENS) + STEPS + BS - 1) // BS
+    tables = (torch.arange(B * nb, dtype=torch.int32) + 1).view(B, nb)
+    k = torch.zeros(cfg.num_layers, B * nb + 1, m.n_kv, BS, m.hd, dtype=torch.bfloat16, device="cuda")
+    v = torch.zeros(cfg.num_layers, B * nb + 1, m.n_kv, m.hd, BS, dtype=torch.bfloat16, device="cuda")
+    gen = torch.Generator().manual_seed(11)
+    toks, pos, slots, q_start, tiles = [], [], [], [0], []
+    for r, n in enumerate(LENS):
+        toks += torch.randint(0, min(cfg.vocab_size, 30000), (n,), generator=gen).tolist()
+        p = torch.arange(n)
+        pos.append(p)
+        slots.append(tables[r].long()[p // BS] * BS + p % BS)
+        for t in range(q_start[-1], q_start[-1] + n, 64):
+            tiles.append((r, t, min(t + 64, q_start[-1] + n)))
+        q_start.append(q_start[-1] + n)
+    i32 = torch.int32
+    meta = AttnMeta(positions=torch.cat(pos).to(i32).cuda(), slots=torch.cat(slots).to(i32).cuda(),
+                    block_tables=tables.cuda(), seq_lens=torch.tensor(LENS, dtype=i32).cuda(),
+                    q_start=torch.tensor(q_start, dtype=i32).cuda(), max_q_len=max(LENS),
+                    logits_idx=torch.tensor([q - 1 for q in q_start[1:]]).cuda(),
+                    tiles=torch.tensor(tiles, dtype=i32).cuda())
+    outs, picks = [], []
+    logits = m.forward(torch.tensor(toks, dtype=i32).cuda(), meta, k, v).float()
+    for step in range(STEPS + 1):
+        outs.append(logits.cpu())
+        picks.append(logits.argmax(-1).cpu())
+        if step == STEPS:
+            break
+        nxt = forced[step] if forced is not None else picks[-1]
+        p = torch.tensor(LENS) + step
+        dmeta = AttnMeta(positions=p.to(i32).cuda(),
+                         slots=(tables[torch.arange(B), p // BS].long() * BS + p % BS).to(i32).cuda(),
+                         block_tables=tables.cuda(), seq_lens=(p + 1).to(i32).cuda(), decode=True)
+        logits = m.forward(nxt.to(i32).cuda(), dmeta, k, v).float()
+    return outs, picks
+
+
+def _worker(rank, world, port, name, quant, forced_path, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0", BCG_CUSTOM_AR="force", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)
+    from byzantine_consensus_llm_agents_amd.parallel import groups
+    groups.init_distributed("gloo")
+    tpg = groups.tensor_parallel_group(world, custom_allreduce=True)
+    forced = torch.load(forced_path, weights_only=True)
+    outs, _ = _run(name, quant, tpg, forced)
+    calls, err = dict(tpg.custom.calls), tpg.custom.take_error()
+    torch.cuda.synchronize()
+    torch.distributed.barrier()
+    if rank in (0, world - 1):
+        torch.save({"logits": outs, "calls": calls, "err": err}, f"{out}.{rank}")
+    groups.destroy()
+
+
+@pytest.mark.parametrize("name,quant,tp", [("qwen3-32b", None, 4), ("mistral-22b", "fp8", 2)])
+def test_tp_matches_tp1_at_real_shapes(tmp_path, name, quant, tp):
+    ref, picks = _run(name, quant, None)
+    torch.cuda.empty_cache()
+    forced_path = str(tmp_path / "forced.pt")
+    torch.save(picks[:-1], forced_path)
+    out = str(tmp_path / "tp")
+    mp.start_processes(_worker, args=(tp, _free_port(), name, quant, forced_path, out), nprocs=tp, join=True,
+                       start_method="spawn")
+    r0, rl = (torch.load(f"{out}.{r}", weights_only=True) for r in (0, tp - 1))
+    assert not r0["err"] and r0["calls"].get(3, 0) > 0  # the fused all-reduce + add + RMSNorm kernel ran
+    agree, total, worst = 0, 0, 1.0
+    for step, (a, b, c) in enumerate(zip(r0["logits"], rl["logits"], ref)):
+        assert torch.equal(a, b), step  # every rank holds the same activations
+        cos = torch.nn.functional.cosine_similarity(a, c, dim=-1)
+        worst = min(worst, cos.min().item())
+        agree += (a.argmax(-1) == c.argmax(-1)).sum().item()
+        total += a.shape[0]
+    print(f"[tp-real] {name} quant={quant} tp={tp}: min cosine {worst:.5f}, greedy agreement {agree}/{total}, "
+          f"custom all-reduce calls {r0['calls']}")
+    assert worst > (0.995 if quant else 0.999), worst
+    assert agree >= 0.95 * total, (agree, total)
