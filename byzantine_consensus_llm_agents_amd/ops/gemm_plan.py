@@ -30,10 +30,9 @@ from typing import Dict, Optional, Tuple
 TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "engine", "tuned",
                      "hand_gemm.json")
 TILES = ((128, 128), (64, 128), (128, 64), (256, 128), (64, 256), (64, 64), (32, 128),  # csrc/kernels/gemm.hip CFGS
-         (256, 128), (128, 256), (128, 128), (256, 256), (256, 256))
+         (256, 128), (128, 256), (128, 128), (256, 256))
 PP_CFG = 10  # csrc/kernels/gemm_pp.hip: 256 x 256 ping-pong tile, N only a multiple of 16
-RS_CFG = 11  # csrc/kernels/gemm_rs.hip: 256 x 256 register-staged tile, same shape rules
-BIG_CFGS = (PP_CFG, RS_CFG)
+BIG_CFGS = (PP_CFG,)  # 256 x 256 tiles (the register-staged form lost its A/B: csrc/experimental/gemm_rs.hip)
 N_CFGS = len(TILES)
 SPLITS = (1, 2, 3, 4, 6, 8)
 

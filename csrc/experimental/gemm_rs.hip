@@ -1,5 +1,15 @@
 // 256 x 256 x 64 GEMM with REGISTER-staged operands, one wave per SIMD (gfx950).
 //
+// EXPERIMENTAL (tools-only build, tools/build_gemm_variants.sh): correct (the GPU GEMM tests
+// passed with it registered as a tile configuration) but SLOWER than the LDS-DMA ping-pong
+// kernel on every Qwen3-14B shape, 1.10-1.25 vs 1.23-1.28 PF/s at M = 16384 and far behind at
+// the split-K decode shapes (profiles/r3_gemm_rs/).  PMC (profiles/r3_gemm_rs/summary_*.txt,
+// down_proj 16384 x 5120 x 17408): MFMA pipe busy 46 % vs 60 %; the waves sit in issue stalls
+// (SQ_WAIT_INST_ANY 63 % of wave cycles, LDS-issue stalls 13 %) and an LDS instruction costs
+// 2.3x the ping-pong kernel's (SQ_ACTIVE_INST_LDS 156 M vs 67 M for the same instruction
+// count): the 16 ds_write_b128 per K-tile that one wave per SIMD must issue are as expensive
+// as the LDS-DMA pieces they replace, and no partner wave covers them.
+//
 //   C[M, N] = X[M, K] · W[N, K]^T            (bf16 in, fp32 accumulate, bf16 out)
 //
 // The third tile family beside gemm.hip (decode tiles) and gemm_pp.hip (256 x 256

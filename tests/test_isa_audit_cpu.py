@@ -1,4 +1,4 @@
-"""Static audit of the register-staged 256x256 GEMM (csrc/kernels/gemm_rs.hip) on the CPU host.
+"""Static audit of the register-staged 256x256 GEMM (csrc/experimental/gemm_rs.hip) on the CPU host.
 
 Its MFMAs are inline asm with AGPR-pinned accumulators, so hipcc pads no MFMA hazard for
 them and would not notice if an accumulator were spilled: an MFMA result copied or stored
@@ -26,7 +26,7 @@ def asm(tmp_path_factory):
     out = tmp_path_factory.mktemp("isa") / "gemm_rs.s"
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fgpu-flush-denormals-to-zero",
                     "-munsafe-fp-atomics", f"-I{ROOT}/csrc/kernels", "-S", "--cuda-device-only",
-                    f"{ROOT}/csrc/kernels/gemm_rs.hip", "-o", str(out)], check=True, capture_output=True)
+                    f"{ROOT}/csrc/experimental/gemm_rs.hip", "-o", str(out)], check=True, capture_output=True)
     return out.read_text()
 
 

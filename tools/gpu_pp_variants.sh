@@ -11,7 +11,7 @@ for v in ${VARIANTS:-$(ls build | grep '^pp_' | sed 's/^pp_//')}; do
 done | tee gpurun_out/ppv/times.jsonl
 [ -z "$PMC_VARIANTS" ] && exit 0
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-GROUPS_TXT=${PMC_GROUPS:-"SQ_WAVES,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_INSTS_MFMA,SQ_VALU_MFMA_BUSY_CYCLES;SQ_INSTS_LDS,SQ_LDS_BANK_CONFLICT,SQ_ACTIVE_INST_LDS,SQ_WAIT_INST_LDS,SQ_INST_CYCLES_VMEM,GRBM_GUI_ACTIVE;FETCH_SIZE,TCC_HIT_sum"}
+GROUPS_TXT=${PMC_GROUPS:-"SQ_WAVES,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_INSTS_MFMA,SQ_VALU_MFMA_BUSY_CYCLES;SQ_INSTS_LDS,SQ_LDS_BANK_CONFLICT,SQ_ACTIVE_INST_LDS,SQ_WAIT_INST_LDS,SQ_INST_CYCLES_VMEM,GRBM_GUI_ACTIVE;FETCH_SIZE,TCC_HIT_sum;TCC_HIT_sum,TCC_MISS_sum,GRBM_GUI_ACTIVE"}
 for v in $PMC_VARIANTS; do
   i=0
   IFS=';' read -ra GROUPS_ARR <<< "$GROUPS_TXT"
@@ -21,5 +21,5 @@ for v in $PMC_VARIANTS; do
       build/pp_$v ${PMC_SHAPE//,/ } 10 > gpurun_out/ppv/$v.p$i.log 2>&1 || { echo "pass $v/$i failed: $group"; tail -3 gpurun_out/ppv/$v.p$i.log; exit 1; }
     echo "pass $v/$i ok: $group"
   done
-  echo "== $v"; python tools/pmc_summary.py gpurun_out/ppv/$v | grep -A40 gemm_pp | tee gpurun_out/ppv/summary_$v.txt
+  echo "== $v"; python tools/pmc_summary.py gpurun_out/ppv/$v | grep -A40 "gemm_" | tee gpurun_out/ppv/summary_$v.txt
 done
