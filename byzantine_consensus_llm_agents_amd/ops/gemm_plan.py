@@ -145,6 +145,10 @@ class Fp8Plan:
             return None
         else:
             cfg, split = (6 if M <= 32 else 1 if M <= 64 else 0), 1
-        if cfg < 0 or cfg not in self.tiles or cfg in BIG_CFGS or N % self.tiles[cfg][1] or K // 128 < split:
+        if cfg < 0 or cfg not in self.tiles or K // 128 < split:
             return None
-        return (cfg, split)
+        if cfg == PP_CFG:  # 256 x 256 ping-pong fp8 kernel (prefill M): N % 16, 32-bit buffer offsets
+            ok = N % 16 == 0 and M * K < 1 << 32 and N * K < 1 << 32
+        else:
+            ok = N % self.tiles[cfg][1] == 0
+        return (cfg, split) if ok else None

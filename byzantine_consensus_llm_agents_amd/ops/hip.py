@@ -209,7 +209,7 @@ def hip_ops() -> SimpleNamespace:
                 return gemm_nt(x, w, cfg, 0, bias=bias)
         return torch.nn.functional.linear(x, w, bias)
 
-    from .gemm_plan import GemmPlan
+    from .gemm_plan import PP_CFG, GemmPlan
     plan = GemmPlan(lib)
 
     # Split-K arrival counters (one int per output tile; the last-arriving workgroup of a
@@ -396,7 +396,9 @@ def hip_ops() -> SimpleNamespace:
         _req(xs.dtype == torch.float32 and xs.numel() == M and xs.is_contiguous() and ws.dtype == torch.float32
              and ws.numel() == N and ws.is_contiguous(), "gemm_nt_fp8: fp32 scales xs [M], ws [N]")
         bm, bn = plan.tiles[cfg]
-        _req(0 <= cfg < 10 and K % 128 == 0 and N % bn == 0 and 1 <= split_k <= K // 128 and epi in (0, 2),
+        pp = cfg == PP_CFG  # 256 x 256 ping-pong kernel: N only a multiple of 16, 32-bit buffer offsets
+        _req(0 <= cfg <= PP_CFG and K % 128 == 0 and N % (16 if pp else bn) == 0 and 1 <= split_k <= K // 128
+             and epi in (0, 2) and (not pp or (M * K < 1 << 32 and N * K < 1 << 32)),
              f"gemm_nt_fp8: shape {M}x{N}x{K} epi {epi} split {split_k} unsupported by tile {cfg}")
         if out is None:
             out = torch.empty(M, N, dtype=torch.bfloat16, device=xq.device)
@@ -408,7 +410,7 @@ def hip_ops() -> SimpleNamespace:
                  and residual.dtype == torch.bfloat16, "gemm_nt_fp8: residual [M,N] bf16")
         wsp = cnt = None
         if split_k > 1:
-            tiles = (M + bm - 1) // bm * (N // bn)
+            tiles = (M + bm - 1) // bm * ((N + bn - 1) // bn)
             _req(tiles <= (1 << 16), "gemm_nt_fp8: too many output tiles for split-K")
             wsp = torch.empty(tiles * split_k * bm * bn, dtype=torch.float32, device=xq.device)
             cnt = _counters(xq.device)

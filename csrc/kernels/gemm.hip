@@ -432,9 +432,15 @@ BCG_API int bcg_gemm_nt(int cfg, int epi, const void* x, const void* w, const vo
 // epi: 0 = store, 2 = residual + result.  Requirements: K % 128 == 0, K/128 >= split_k,
 // N % BN == 0 (cfg's tile), x_scale [M] / w_scale [N] fp32, pointers 16-B aligned; split-K
 // workspace / counters as bcg_gemm_nt.
+BCG_API int bcg_gemm_pp_fp8(int epi, const void* xq, const void* wq, const float* x_scale, const float* w_scale,
+                            const void* bias, const void* residual, void* c, void* ws, void* counters, int M, int N,
+                            int K, int split_k, hipStream_t stream);
+
 BCG_API int bcg_gemm_nt_fp8(int cfg, int epi, const void* xq, const void* wq, const float* x_scale,
                             const float* w_scale, const void* bias, const void* residual, void* c, void* ws,
                             void* counters, int M, int N, int K, int split_k, hipStream_t stream) {
+  if (cfg == PP_CFG)  // the 256 x 256 ping-pong kernel's fp8 form (prefill M)
+    return bcg_gemm_pp_fp8(epi, xq, wq, x_scale, w_scale, bias, residual, c, ws, counters, M, N, K, split_k, stream);
   if (M <= 0 || K % 128 || K <= 0 || split_k < 1 || K / 128 < split_k || !x_scale || !w_scale) return -2;
   if (split_k > 1 && (!ws || !counters)) return -2;
   if (cfg < 0 || cfg >= N_CFG || N % CFGS[cfg].bn) return -2;

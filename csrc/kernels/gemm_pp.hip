@@ -41,6 +41,17 @@
 //     on one XCD, so each weight byte comes from HBM once;
 //   * split-K: fp32 partial tiles stored write-through (sc1), last arriver reduces
 //     (as gemm.hip, cdna_hip_programming.md §6 Guideline 16 R1).
+//
+// fp8 variant (F8; BASELINE config 5's prefill projections): e4m3fn operands, a row-wise
+// activation scale and a per-output-channel weight scale applied in the epilogue
+//   C[m, n] = xs[m] * ws[n] * sum_k Xq[m, k] Wq[n, k]   (+ bias, + residual).
+// A K-tile is then 128 elements in the SAME 128-B LDS rows, i.e. the same LDS-DMA bytes and
+// fragment reads per K-tile as bf16; each block's two 16-B fragments (chunks fq and 4 + fq)
+// are the 32-byte operand of ONE v_mfma_scale_f32_16x16x128_f8f6f4 (unit E8M0 scales; A and B
+// share the lane -> k map, so the permuted k order inside the instruction cancels), which
+// takes the cycles of two bf16 16x16x32 MFMAs for 4x their K: twice the FLOPs per K-tile.
+#include <type_traits>
+
 #include "common.h"
 
 #ifndef PP_GLDS_IN_MFMA
@@ -74,11 +85,15 @@ constexpr int HALF = 128 * 128;  // one half slot: 128 rows x 128 B
 // into ring slot n % RING.  A wait before phase r's first barrier covers the loads of phases
 // <= r - DEPTH; a load of phase p is then visible to the readers of phase >= p + DEPTH + 1
 // (RAW: DEPTH <= LEAD - 2), and a slot is refilled >= 2 phases after its last read (WAR:
-// RING >= LEAD + 1).
+// RING >= LEAD + 1).  The fp8 variant reads A-lo(t) in phase j0 beside B-lo(t) (phase n for
+// that kind: no A operand is carried across K-tiles, which keeps its 8-register operands in
+// place) and so loads one phase later (LEAD - 1; WAR then RING >= LEAD + 2).
 enum { K_ALO = 0, K_BLO = 1, K_BHI = 2, K_AHI = 3 };
 constexpr int RING = PP_RING, LEAD = PP_LEAD, DEPTH = LEAD - 2;
 static_assert(RING >= LEAD + 1 && DEPTH >= 2 && 2 * DEPTH <= 62 && RING * HALF <= 160 * 1024, "ring geometry");
 enum Epilogue { EPI_STORE = 0, EPI_SILU_MUL = 1, EPI_RESIDUAL = 2 };
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
@@ -95,12 +110,19 @@ __device__ __forceinline__ void sbar() {
 #endif
 }
 
-template <int EPI>
+template <int EPI, bool F8 = false>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
-    const bf16_t* __restrict__ X, const bf16_t* __restrict__ W, const bf16_t* __restrict__ bias,
+    const void* __restrict__ Xv, const void* __restrict__ Wv, const bf16_t* __restrict__ bias,
     const bf16_t* __restrict__ residual, bf16_t* __restrict__ C, float* __restrict__ ws,
     int* __restrict__ counters, int M, int N, int K, int ldc, int inter, int m_tiles, int n_tiles,
-    int split_k) {
+    int split_k, const float* __restrict__ x_scale, const float* __restrict__ w_scale) {
+  static_assert(!F8 || EPI != EPI_SILU_MUL, "fp8: store / residual epilogues");
+  constexpr int ESZ = F8 ? 1 : 2;   // bytes per element
+  constexpr int KT = 128 / ESZ;     // K elements per K-tile (one 128-B LDS row)
+  constexpr int LEAD = F8 ? ::LEAD - 1 : ::LEAD, DEPTH = LEAD - 2;
+  static_assert(DEPTH >= 2 && RING >= LEAD + 1 + (F8 ? 1 : 0), "ring geometry");
+  const unsigned char* X = static_cast<const unsigned char*>(Xv);
+  const unsigned char* W = static_cast<const unsigned char*>(Wv);
   // ONE shared array (a second __shared__ object can make hipcc drain vmcnt before every
   // ds_read: cdna_hip_programming.md "Projection GEMM" item 4a)
   __shared__ __attribute__((aligned(1024))) unsigned char smem[RING * HALF];
@@ -119,7 +141,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
   const int gm = min(m_tiles - grp * PP_GROUP_M, PP_GROUP_M);
   const int m_tile = grp * PP_GROUP_M + in_grp % gm, n_tile = in_grp / gm;
   const int m0 = m_tile * PBM, n0 = n_tile * PBN;
-  const int nk_all = K / PBK;
+  const int nk_all = K / KT;
   const int kt0 = split * nk_all / split_k;
   const int nk = (split + 1) * nk_all / split_k - kt0;
 
@@ -140,7 +162,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
   // each thread stages 2 x 16 B of a half slot: rows (wave*2 + i)*8 + lane/8, chunk slot lane%8
   const int st_r0 = wave * 16 + (lane >> 3);
   const int st_phys = lane & 7;
-  uint32_t offA[2][2], offB[2][2];  // [hi][i]: element offsets of the rows (k offset added per tile)
+  uint32_t offA[2][2], offB[2][2];  // [hi][i]: byte offsets of the rows (k offset added per tile)
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int s = st_r0 + i * 8;
@@ -148,31 +170,32 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
 #pragma unroll
     for (int hi = 0; hi < 2; ++hi) {
       const int am = min(m0 + (s >> 6) * 128 + hi * 64 + (s & 63), M - 1);
-      offA[hi][i] = static_cast<uint32_t>(am) * K + c * 8;
+      offA[hi][i] = static_cast<uint32_t>(am) * K * ESZ + c * 16;
       const int bn = w_row((s >> 5) * 64 + hi * 32 + (s & 31));
-      offB[hi][i] = static_cast<uint32_t>(bn) * K + c * 8;
+      offB[hi][i] = static_cast<uint32_t>(bn) * K * ESZ + c * 16;
     }
   }
   const int nhalf = 4 * nk;  // half-tiles of this workgroup's K range
   // buffer descriptors (byte ranges < 4 GiB: checked by the host wrapper)
-  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(X), 0,
-                                                                       static_cast<uint32_t>(M) * K * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(X), 0,
+                                                                       static_cast<uint32_t>(M) * K * ESZ, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(W), 0, static_cast<uint32_t>(EPI == EPI_SILU_MUL ? 2 * inter : N) * K * 2, 0x00020000);
+      const_cast<unsigned char*>(W), 0, static_cast<uint32_t>(EPI == EPI_SILU_MUL ? 2 * inter : N) * K * ESZ,
+      0x00020000);
   // glds piece i of half-tile n (kind = n & 3, K-tile n >> 2) into ring slot `slot`
   auto load_piece = [&](int n, int kind, int slot, int i) {
 #ifdef PP_ABL_NOLOAD
     if (n >= 8) return;
 #endif
     unsigned char* dst = smem + slot * HALF + wave * 2048 + i * 1024;
-    const uint32_t k0 = (kt0 + (n >> 2)) * PBK;
+    const uint32_t k0 = (kt0 + (n >> 2)) * 128;  // bytes
     const uint32_t* off = kind == K_ALO ? offA[0] : kind == K_AHI ? offA[1] : kind == K_BLO ? offB[0] : offB[1];
     if constexpr (PP_BUFFER_LDS) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds((kind == K_ALO || kind == K_AHI) ? rsX : rsW,
-                                               (__attribute__((address_space(3))) void*)dst, 16, off[i] * 2, k0 * 2,
+                                               (__attribute__((address_space(3))) void*)dst, 16, off[i], k0,
                                                0, 0);
     } else {
-      const bf16_t* base = (kind == K_ALO || kind == K_AHI) ? X : W;
+      const unsigned char* base = (kind == K_ALO || kind == K_AHI) ? X : W;
       __builtin_amdgcn_global_load_lds(base + (off[i] + k0), dst, 16, 0, 0);
     }
   };
@@ -189,57 +212,87 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
 
   // [block][k-step]; alo/ahi: A-lo / A-hi fragments (A-lo of tile t+1 is read in phase j3 of
   // tile t, beside that phase's MFMAs on A-hi: per-phase reads 4, 4, 8, 8 instead of 12, 4, 8, 0)
-  bf16x8 alo[4][2], ahi[4][2], blo[2][2], bhi[2][2];
-  auto read_a = [&](int t, int slot, bf16x8 (&a)[4][2]) {
-#ifdef PP_ABL_NOREAD
-    if (t >= 1) return;
-#endif
-    const unsigned char* base = smem + slot * HALF;
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int r = g * 64 + mb * 16 + fr;
-        a[mb][s] = *reinterpret_cast<const bf16x8*>(base + r * 128 + swz(r, 4 * s + fq) * 16);
-      }
+  // (fp8: a block's two fragments are the two halves of ONE 8-register MFMA operand, read
+  // straight into it -- separate halves cost a copy per MFMA and spill)
+  using Frag = std::conditional_t<F8, i32x8, bf16x8[2]>;
+  Frag alo[4], ahi[4], blo[2], bhi[2];
+  // whole-operand definition (a half-vector store would keep the old operand alive)
+  auto put = [](Frag& f, bf16x8 v0, bf16x8 v1) {
+    if constexpr (F8) {
+      f = __builtin_shufflevector(__builtin_bit_cast(i32x4, v0), __builtin_bit_cast(i32x4, v1), 0, 1, 2, 3, 4, 5,
+                                  6, 7);
+    } else {
+      f[0] = v0;
+      f[1] = v1;
+    }
   };
-  auto read_b = [&](int t, int slot, bf16x8 (&b)[2][2]) {
+  auto read_a = [&](int t, int slot, Frag (&a)[4]) {
 #ifdef PP_ABL_NOREAD
     if (t >= 1) return;
 #endif
     const unsigned char* base = smem + slot * HALF;
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
+    for (int mb = 0; mb < 4; ++mb) {
+      const int r = g * 64 + mb * 16 + fr;
+      put(a[mb], *reinterpret_cast<const bf16x8*>(base + r * 128 + swz(r, fq) * 16),
+          *reinterpret_cast<const bf16x8*>(base + r * 128 + swz(r, 4 + fq) * 16));
+    }
+  };
+  auto read_b = [&](int t, int slot, Frag (&b)[2]) {
+#ifdef PP_ABL_NOREAD
+    if (t >= 1) return;
+#endif
+    const unsigned char* base = smem + slot * HALF;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int r = wc * 32 + nb * 16 + fr;
-        b[nb][s] = *reinterpret_cast<const bf16x8*>(base + r * 128 + swz(r, 4 * s + fq) * 16);
-      }
+    for (int nb = 0; nb < 2; ++nb) {
+      const int r = wc * 32 + nb * 16 + fr;
+      put(b[nb], *reinterpret_cast<const bf16x8*>(base + r * 128 + swz(r, fq) * 16),
+          *reinterpret_cast<const bf16x8*>(base + r * 128 + swz(r, 4 + fq) * 16));
+    }
   };
   // 16 MFMAs of one quadrant; with PP_GLDS_IN_MFMA the phase's two glds pieces (K-tile lt,
   // half lslot; lt < 0: none) go between them, where the wave waits on the MFMA pipe anyway
-  auto mfma = [&](int nh, int mh, const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2], int ln, int lkind,
+  auto mfma = [&](int nh, int mh, const Frag (&a)[4], const Frag (&b)[2], int ln, int lkind,
                   int lslot) {
 #ifndef PP_NO_SETPRIO
     __builtin_amdgcn_s_setprio(1);
 #endif
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
+    if constexpr (F8) {  // 8 block-scaled K = 128 MFMAs, each over both 16-B fragments of a block
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) {
-          acc[nh * 2 + nb][mh * 4 + mb] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nb][s], a[mb][s], acc[nh * 2 + nb][mh * 4 + mb], 0, 0, 0);
+          // formats 0/0 = e4m3 x e4m3; E8M0 scale 127 = 1.0 for both operands
+          acc[nh * 2 + nb][mh * 4 + mb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              b[nb], a[mb], acc[nh * 2 + nb][mh * 4 + mb], 0, 0, 0, 127, 0, 127);
           if constexpr (PP_GLDS_IN_MFMA) {
-            const int idx = (s * 2 + nb) * 4 + mb;
-            if (idx == PP_PIECE0 || idx == PP_PIECE1) {
+            const int idx = nb * 4 + mb;
+            if (idx == PP_PIECE0 / 2 || idx == PP_PIECE1 / 2) {
               __builtin_amdgcn_sched_barrier(0);
-              if (ln >= 0) load_piece(ln, lkind, lslot, idx == PP_PIECE1);
+              if (ln >= 0) load_piece(ln, lkind, lslot, idx == PP_PIECE1 / 2);
               __builtin_amdgcn_sched_barrier(0);
             }
           }
         }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+          for (int mb = 0; mb < 4; ++mb) {
+            acc[nh * 2 + nb][mh * 4 + mb] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nb][s], a[mb][s], acc[nh * 2 + nb][mh * 4 + mb], 0, 0, 0);
+            if constexpr (PP_GLDS_IN_MFMA) {
+              const int idx = (s * 2 + nb) * 4 + mb;
+              if (idx == PP_PIECE0 || idx == PP_PIECE1) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (ln >= 0) load_piece(ln, lkind, lslot, idx == PP_PIECE1);
+                __builtin_amdgcn_sched_barrier(0);
+              }
+            }
+          }
+    }
 #ifndef PP_NO_SETPRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
@@ -259,7 +312,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     }
   };
   // one phase: [read turn done by the caller] wait, barrier, MFMAs (+ this phase's load), barrier
-  auto phase = [&](bool window, int nh, int mh, const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2], int ln,
+  auto phase = [&](bool window, int nh, int mh, const Frag (&a)[4], const Frag (&b)[2], int ln,
                    int lkind, int lslot) {
     if constexpr (!PP_GLDS_IN_MFMA) {
       if (ln >= 0) load_half(ln, lkind, lslot);
@@ -283,7 +336,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
   }
   sbar();
   if (g == 1) sbar();  // group 1 runs one barrier behind group 0
-  read_a(0, 0, alo);   // A-lo(0) = half-tile 0, slot 0 ("phase -1")
+  if constexpr (!F8) read_a(0, 0, alo);  // A-lo(0) = half-tile 0, slot 0 ("phase -1")
 
   int ls = LEAD % RING, rs = 1;  // ring slots of the next load (n = p + LEAD) and read (n = p + 1)
   auto bump = [](int& x) { x = x + 1 == RING ? 0 : x + 1; };
@@ -293,7 +346,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     auto ln = [&](int j) { return p0 + j + LEAD < nhalf ? p0 + j + LEAD : -1; };
     // wait windows: read-turn loads -> phase r has a load; loads among MFMAs -> phase r-1 has one
     auto win = [&](int j) { return (p0 + j + LEAD - (PP_GLDS_IN_MFMA ? 1 : 0)) < nhalf; };
-    // j0: read B-lo(t)
+    // j0: read B-lo(t) (fp8: and A-lo(t), the slot before)
+    if constexpr (F8) read_a(t, rs == 0 ? RING - 1 : rs - 1, alo);
     read_b(t, rs, blo);
     phase(win(0), 0, 0, alo, blo, ln(0), (0 + LEAD) & 3, ls);
     bump(ls), bump(rs);
@@ -306,7 +360,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     phase(win(2), 1, 1, ahi, bhi, ln(2), (2 + LEAD) & 3, ls);
     bump(ls), bump(rs);
     // j3: read A-lo(t+1)
-    if (t + 1 < nk) read_a(t + 1, rs, alo);
+    if (!F8 && t + 1 < nk) read_a(t + 1, rs, alo);
     phase(win(3), 0, 1, ahi, blo, ln(3), (3 + LEAD) & 3, ls);
     bump(ls), bump(rs);
   }
@@ -371,6 +425,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
         const int n = n0 + wc * 64 + nb * 16 + 4 * fq;
         if (n >= N) continue;
         float v[4] = {acc[nb][mb][0], acc[nb][mb][1], acc[nb][mb][2], acc[nb][mb][3]};
+        if constexpr (F8) {  // dequantise: row scale x column scales
+          const float xs = x_scale[m];
+          const f32x4 wsc = *reinterpret_cast<const f32x4*>(w_scale + n);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] *= xs * wsc[e];
+        }
         if (bias != nullptr) {
           const u16x4 b = *reinterpret_cast<const u16x4*>(bias + n);
 #pragma unroll
@@ -390,15 +450,15 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
   }
 }
 
-template <int EPI>
+template <int EPI, bool F8 = false>
 int launch_pp(const void* x, const void* w, const void* bias, const void* res, void* c, float* ws, int* cnt, int M,
-              int N, int K, int inter, int split_k, hipStream_t stream) {
+              int N, int K, int inter, int split_k, hipStream_t stream, const float* xs = nullptr,
+              const float* wsc = nullptr) {
   const int m_tiles = (M + PBM - 1) / PBM, n_tiles = (N + PBN - 1) / PBN;
   const int ldc = EPI == EPI_SILU_MUL ? inter : N;
-  hipLaunchKernelGGL((gemm_pp_kernel<EPI>), dim3(m_tiles * n_tiles * split_k), dim3(512), 0, stream,
-                     static_cast<const bf16_t*>(x), static_cast<const bf16_t*>(w), static_cast<const bf16_t*>(bias),
-                     static_cast<const bf16_t*>(res), static_cast<bf16_t*>(c), ws, cnt, M, N, K, ldc, inter, m_tiles,
-                     n_tiles, split_k);
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, F8>), dim3(m_tiles * n_tiles * split_k), dim3(512), 0, stream, x, w,
+                     static_cast<const bf16_t*>(bias), static_cast<const bf16_t*>(res), static_cast<bf16_t*>(c), ws,
+                     cnt, M, N, K, ldc, inter, m_tiles, n_tiles, split_k, xs, wsc);
   return BCG_CHECK_LAUNCH();
 }
 
@@ -423,6 +483,30 @@ BCG_API int bcg_gemm_pp(int epi, const void* x, const void* w, const void* bias,
     case EPI_RESIDUAL:
       if (!residual) return -2;
       return launch_pp<EPI_RESIDUAL>(x, w, bias, residual, c, wsf, cnt, M, N, K, inter, split_k, stream);
+    default: return -2;
+  }
+}
+
+// fp8 (e4m3fn) prefill projection: C = x_scale[m] * w_scale[n] * (Xq . Wq^T) (+ bias) (+ residual).
+// epi: 0 = store, 2 = residual + result.  K % 128 == 0, K/128 >= split_k; N % 16 == 0 (a partial
+// last n-tile is masked); x_scale [M] / w_scale [N] fp32; split-K workspace as bcg_gemm_pp.
+BCG_API int bcg_gemm_pp_fp8(int epi, const void* xq, const void* wq, const float* x_scale, const float* w_scale,
+                            const void* bias, const void* residual, void* c, void* ws, void* counters, int M, int N,
+                            int K, int split_k, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || N % 16 || K % 128 || K <= 0 || split_k < 1 || K / 128 < split_k) return -2;
+  if (!x_scale || !w_scale) return -2;
+  if (1ull * M * K >= (1ull << 32) || 1ull * N * K >= (1ull << 32)) return -2;  // 32-bit buffer offsets
+  if (split_k > 1 && (!ws || !counters)) return -2;
+  float* wsf = static_cast<float*>(ws);
+  int* cnt = static_cast<int*>(counters);
+  switch (epi) {
+    case EPI_STORE:
+      return launch_pp<EPI_STORE, true>(xq, wq, bias, residual, c, wsf, cnt, M, N, K, 0, split_k, stream, x_scale,
+                                        w_scale);
+    case EPI_RESIDUAL:
+      if (!residual) return -2;
+      return launch_pp<EPI_RESIDUAL, true>(xq, wq, bias, residual, c, wsf, cnt, M, N, K, 0, split_k, stream, x_scale,
+                                           w_scale);
     default: return -2;
   }
 }

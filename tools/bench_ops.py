@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--ctx", type=int, default=1700)
     ap.add_argument("--tunable", action="store_true", help="PyTorch TunableOp for the hipBLASLt GEMMs")
     ap.add_argument("--skip-gemm", action="store_true")
+    ap.add_argument("--share", type=int, default=1,
+                    help="decode attention: rows in groups of this many map the same first 16 KV blocks "
+                         "(the prefix cache's shared system-prompt blocks)")
     args = ap.parse_args()
     if args.tunable:
         torch.cuda.tunable.enable(True)
@@ -74,12 +77,15 @@ def main():
         nb = (args.ctx + 15) // 16
         assert B * nb + 1 <= NB
         tables = (torch.arange(B * nb, dtype=torch.int32, device="cuda").view(B, nb) + 1)
+        if args.share > 1:  # every row of a group maps the group leader's first 16 blocks
+            lead = (torch.arange(B, device="cuda") // args.share) * args.share
+            tables[:, :16] = tables[lead, :16]
         tables = torch.cat([tables, torch.zeros(B, 512 - nb, dtype=torch.int32, device="cuda")], 1).contiguous()
         seq = torch.full((B,), args.ctx, dtype=torch.int32, device="cuda")
         q = torch.randn(B, cfg.num_heads, hd, device="cuda", dtype=torch.bfloat16)
         t = timeit(lambda: hip.paged_attention_decode(q, k, v, 0, tables, seq, hd ** -0.5))
         gb = B * args.ctx * cfg.num_kv_heads * hd * 2 * 2 / 1e9
-        rec = {"B": B, "ctx": args.ctx, "us": round(t, 1), "TBps": round(gb / t * 1e3, 2)}
+        rec = {"B": B, "ctx": args.ctx, "share": args.share, "us": round(t, 1), "TBps": round(gb / t * 1e3, 2)}
         out["attention"].append(rec)
         print(json.dumps(rec), flush=True)
     # fused QK-norm + RoPE + paged KV write (decode rows and a prefill chunk)

@@ -13,8 +13,11 @@ if [ -z "$SKIP_TESTS" ]; then
   grep -E "tp-real|passed|failed" gpurun_out/tp/tests.log | tail -5
 fi
 COMMON="--one-device --steps ${STEPS:-4} --warmup 1 --fill-max-s 150 --deadline-s 1500"
+# TP = 4: collectives on gloo, eager decode (4 processes on one GPU are not co-resident: a
+# spinning xGMI all-reduce would wait on a descheduled peer -- tests/test_tp_real_shapes_gpu.py)
 echo "== Qwen3-32B TP=4, 8h+2b"
 timeout -k 10 900 python bench.py --gpus 4 --tp 4 --model qwen3-32b --sims-per-gpu 16 --max-batch-seqs 160 \
+  --no-custom-allreduce --no-graphs \
   --kv-cache-gb 6 $COMMON > gpurun_out/tp/tp4_qwen3_32b.json 2> gpurun_out/tp/tp4_qwen3_32b.err \
   || { tail -30 gpurun_out/tp/tp4_qwen3_32b.err; exit 1; }
 cat gpurun_out/tp/tp4_qwen3_32b.json
