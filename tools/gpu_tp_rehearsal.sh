@@ -1,28 +1,28 @@
 #!/bin/bash
 # Configs 4 and 5 at real shapes on ONE GPU (ranks share cuda:0; gloo + the xGMI all-reduce kernels
-# forced over IPC peer buffers): the real-shape TP numerics tests, then the bench pool through the
-# TP engine (driver/follower plans, decode graphs with the custom all-reduce inside) -- the
-# plan-exchange cost is in detail.phases_rank0 (plan_exchange).  Rehearsal only: N ranks on one
-# GPU time-share it, so the decisions/s here are not a measurement.
+# forced over IPC peer buffers): the real-shape TP numerics tests (TP = 4 on gloo collectives,
+# TP = 2 on the xGMI kernels), then the bench pool through the TP = 2 engine (driver/follower
+# plans, decode graphs with the all-reduce inside; BCG_AR_CAP_MB raised so that prefill chunks
+# also take the xGMI kernel instead of gloo host copies).  The plan-exchange cost is in
+# detail.phases_rank0 (plan_exchange).  Rehearsal only: the ranks time-share one GPU, so the
+# decisions/s here are not a measurement.  (TP = 4 engine runs need 4 co-resident ranks: only on
+# a node with one GPU per rank, see tests/test_tp_real_shapes_gpu.py.)
 set -o pipefail
 mkdir -p gpurun_out/tp
-export HSA_ENABLE_IPC_MODE_LEGACY=0
+export HSA_ENABLE_IPC_MODE_LEGACY=0 BCG_AR_CAP_MB=512
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 600 python -u -m pytest -x -v -rP --timeout 540 --timeout-method thread tests/test_tp_real_shapes_gpu.py \
     > gpurun_out/tp/tests.log 2>&1 || { tail -40 gpurun_out/tp/tests.log; exit 1; }
   grep -E "tp-real|passed|failed" gpurun_out/tp/tests.log | tail -5
 fi
-COMMON="--one-device --steps ${STEPS:-4} --warmup 1 --fill-max-s 150 --deadline-s 1500"
-# TP = 4: collectives on gloo, eager decode (4 processes on one GPU are not co-resident: a
-# spinning xGMI all-reduce would wait on a descheduled peer -- tests/test_tp_real_shapes_gpu.py)
-echo "== Qwen3-32B TP=4, 8h+2b"
-timeout -k 10 900 python bench.py --gpus 4 --tp 4 --model qwen3-32b --sims-per-gpu 16 --max-batch-seqs 160 \
-  --no-custom-allreduce --no-graphs \
-  --kv-cache-gb 6 $COMMON > gpurun_out/tp/tp4_qwen3_32b.json 2> gpurun_out/tp/tp4_qwen3_32b.err \
-  || { tail -30 gpurun_out/tp/tp4_qwen3_32b.err; exit 1; }
-cat gpurun_out/tp/tp4_qwen3_32b.json
+COMMON="--one-device --steps ${STEPS:-4} --warmup 1 --fill-max-s 120 --deadline-s 1500"
+echo "== Qwen3-32B TP=2, 8h+2b"
+timeout -k 10 600 python bench.py --gpus 2 --tp 2 --model qwen3-32b --sims-per-gpu 16 --max-batch-seqs 160 \
+  --kv-cache-gb 12 $COMMON > gpurun_out/tp/tp2_qwen3_32b.json 2> gpurun_out/tp/tp2_qwen3_32b.err \
+  || { tail -30 gpurun_out/tp/tp2_qwen3_32b.err; exit 1; }
+cat gpurun_out/tp/tp2_qwen3_32b.json
 echo "== Mistral-22B fp8 TP=2, 16h+4b"
-timeout -k 10 900 python bench.py --gpus 2 --tp 2 --model mistral-22b --quantization fp8 --honest 16 --byzantine 4 \
+timeout -k 10 600 python bench.py --gpus 2 --tp 2 --model mistral-22b --quantization fp8 --honest 16 --byzantine 4 \
   --sims-per-gpu 8 --max-batch-seqs 160 --kv-cache-gb 8 $COMMON > gpurun_out/tp/tp2_mistral22b_fp8.json \
   2> gpurun_out/tp/tp2_mistral22b_fp8.err || { tail -30 gpurun_out/tp/tp2_mistral22b_fp8.err; exit 1; }
 cat gpurun_out/tp/tp2_mistral22b_fp8.json
