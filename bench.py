@@ -8,9 +8,16 @@ Unit of work.  ``--sims-per-gpu`` independent games (seeds) run continuously
 on each engine, each on its own thread; a game that ends is replaced by a
 fresh seed, so the continuously-batched decode stays full (steady state).  One
 "step" is one fixed wall-clock window of ``--window-s`` seconds of that pool;
-its decisions are the accepted decide/vote outputs completed inside it.  W
-warmup windows bring the pool to steady state (full batch, warm prefix cache,
-every decode graph captured), then K windows are timed between a barrier +
+its decisions are the accepted decide/vote outputs completed inside it.
+
+Steady state of WHOLE games ("wall-clock covers full simulations"): a
+fresh pool would put every game in its first rounds at once (short prompts), so
+each slot's first game is first burned in for A ~ Geometric(``--age-p``) rounds on
+a scripted CPU engine (``SimPool.burn_in``: the age law of a long-running pool),
+the pool then runs until every slot has finished a decide phase (``--fill-max-s``;
+the start-up prefill wave is over) -- this fill counts toward the W warmup windows
+(full batch, warm prefix cache, every decode graph captured) -- and K windows are
+timed between a barrier +
 ``torch.cuda.synchronize()`` on both sides; the elapsed time is the max over
 ranks and the decision count the sum over DP replicas.  Nothing is skipped
 inside the timed region: every decision counted was fully generated,
@@ -72,9 +79,9 @@ def parse(argv=None):
     ap.add_argument("--burnin-chars", default="320,420",
                     help="internal_strategy,public_reasoning characters of the burn-in outputs "
                          "(measured means of the engine's outputs: detail.age_mix.output_chars)")
-    ap.add_argument("--fill-max-s", type=float, default=240.0,
-                    help="before the warmup windows, wait (at most this long) until every game has "
-                         "finished its first decide phase: the start-up prefill wave is over")
+    ap.add_argument("--fill-max-s", type=float, default=200.0,
+                    help="wait (at most this long) until every game has finished its first decide "
+                         "phase: the start-up prefill wave is over; the fill counts toward the warmup windows")
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--max-rounds", type=int, default=50)
     ap.add_argument("--seed", type=int, default=1234)
@@ -366,9 +373,11 @@ def main(argv=None):
             time.sleep(0.5)
     fill_s = time.perf_counter() - t_fill
     barrier()
-    time.sleep(args.window_s * args.warmup)
+    # W warmup windows of pool time: a fill that already ran that long counts toward them
+    time.sleep(max(0.0, args.window_s * args.warmup - fill_s))
     if rank == 0:
-        print(f"[warmup] fill {fill_s:.1f}s + {args.warmup} x {args.window_s}s windows, accepted={accepted()} "
+        print(f"[warmup] fill {fill_s:.1f}s, warmup {max(fill_s, args.warmup * args.window_s):.1f}s "
+              f"(>= {args.warmup} x {args.window_s}s windows), accepted={accepted()} "
               f"init={init_s:.1f}s", file=sys.stderr, flush=True)
 
     eng = getattr(llm.backend, "stats", {})
