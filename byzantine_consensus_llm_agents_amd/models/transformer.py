@@ -47,17 +47,30 @@ class TPGroup:
     ``custom`` (optional): an xGMI peer-memory all-reduce
     (``parallel.custom_allreduce.XGMIAllReduce``) used for every message it
     accepts -- the decode-sized ones; the rest go through RCCL.
+    ``chunk_large``: messages beyond the custom kernel's cap go through it in cap-sized
+    pieces instead of the process group -- set when that group is gloo (ranks sharing one
+    GPU: a gloo all-reduce of a prefill chunk is a host round trip per call).
     """
 
-    def __init__(self, group=None, rank: int = 0, size: int = 1, custom=None, ctrl=None, leader: int = 0):
+    def __init__(self, group=None, rank: int = 0, size: int = 1, custom=None, ctrl=None, leader: int = 0,
+                 chunk_large: bool = False):
         self.group, self.rank, self.size, self.custom = group, rank, size, custom
         self.ctrl = ctrl        # CPU (gloo) group of the same ranks: the driver's plan broadcasts
         self.leader = leader    # global rank of this group's rank 0 (the driver)
+        self.chunk_large = chunk_large
+
+    def _chunkable(self, x: torch.Tensor) -> bool:
+        return (self.chunk_large and self.custom is not None and x.dtype == torch.bfloat16
+                and x.is_contiguous() and x.numel() % 8 == 0)
 
     def all_reduce_(self, x: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
             if self.custom is not None and self.custom.can(x):
                 self.custom.all_reduce_(x)
+            elif self._chunkable(x):
+                flat, step = x.view(-1), (self.custom.cap_bytes // 2) // 8 * 8
+                for i in range(0, flat.numel(), step):
+                    self.custom.all_reduce_(flat[i:i + step])
             else:
                 torch.distributed.all_reduce(x, group=self.group)
         return x
@@ -66,9 +79,15 @@ class TPGroup:
                                eps: float, ops):
         """(rmsnorm(residual + sum_ranks x) * w, updated residual): the row-parallel projection's
         all-reduce fused with the next residual add + RMSNorm where the xGMI kernel takes it."""
-        if (self.size > 1 and residual is not None and self.custom is not None
-                and self.custom.can_addnorm(x) and x.is_cuda):
-            return self.custom.all_reduce_add_rmsnorm(x, residual, w, eps), residual
+        if self.size > 1 and residual is not None and self.custom is not None and x.is_cuda:
+            if self.custom.can_addnorm(x):
+                return self.custom.all_reduce_add_rmsnorm(x, residual, w, eps), residual
+            if x.dim() == 2 and self._chunkable(x) and residual.is_contiguous():
+                rows = max(1, self.custom.cap_bytes // (2 * x.shape[1]))
+                if self.custom.can_addnorm(x[:rows]):
+                    h = torch.cat([self.custom.all_reduce_add_rmsnorm(x[r:r + rows], residual[r:r + rows], w, eps)
+                                   for r in range(0, x.shape[0], rows)])
+                    return h, residual
         return ops.add_rmsnorm(self.all_reduce_(x), residual, w, eps)
 
     def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
@@ -80,12 +99,13 @@ class TPGroup:
             # small gathers (decode logits of a few rows) over the xGMI kernel: every rank
             # places its shard in a zeroed full-width tensor and the shards are summed --
             # exact (x + 0), graph-capturable, no RCCL call inside a captured decode step
+            # (beyond the kernel's cap: in pieces when the group is gloo -- graph capture
+            # cannot hold a gloo collective)
             full = torch.zeros(full_shape, dtype=x.dtype, device=x.device)
-            if self.custom.can(full):
+            if self.custom.can(full) or self._chunkable(full):
                 w_ = x.shape[-1]
                 full[..., self.rank * w_:(self.rank + 1) * w_].copy_(x)
-                self.custom.all_reduce_(full)
-                return full
+                return self.all_reduce_(full)
         parts = [torch.empty_like(x) for _ in range(self.size)]
         torch.distributed.all_gather(parts, x, group=self.group)
         return torch.cat(parts, dim=-1)

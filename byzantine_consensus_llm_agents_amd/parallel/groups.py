@@ -118,13 +118,13 @@ def tensor_parallel_group(tp: int, custom_allreduce: bool = False) -> TPGroup:
     if custom_allreduce and mode != "0" and (mode == "force" or dist.get_backend(_TP_GROUPS[tp]) == "nccl"):
         if tp not in _CUSTOM_AR:
             from .custom_allreduce import XGMIAllReduce
-            # BCG_AR_CAP_MB: largest message of the xGMI kernels (RCCL above it); a one-GPU
-            # rehearsal raises it so prefill chunks do not fall back to gloo host copies
+            # BCG_AR_CAP_MB: largest message of the xGMI kernels (RCCL above it; over gloo the
+            # larger messages go through the kernels in cap-sized pieces, TPGroup.chunk_large)
             _CUSTOM_AR[tp] = XGMIAllReduce(_TP_GROUPS[tp], cap_bytes=int(os.environ.get("BCG_AR_CAP_MB", "32")) << 20,
                                            timeout_s=float(os.environ.get("BCG_AR_TIMEOUT_S", "30")))
         custom = _CUSTOM_AR[tp]
     return TPGroup(_TP_GROUPS[tp], lay.tp_rank, tp, custom=custom, ctrl=_TP_CTRL[tp],
-                   leader=lay.rank - lay.tp_rank)
+                   leader=lay.rank - lay.tp_rank, chunk_large=dist.get_backend(_TP_GROUPS[tp]) == "gloo")
 
 
 def data_parallel_group(tp: int):

@@ -61,6 +61,26 @@ def test_tp_group_dispatch(monkeypatch):
     assert fake.calls == 1 and seen == ["pg"]
 
 
+def test_tp_group_chunks_large_messages_over_gloo(monkeypatch):
+    """chunk_large (TP group on gloo): a message above the kernel's cap goes through it in
+    cap-sized pieces, never through the process group."""
+    seen = []
+    monkeypatch.setattr(torch.distributed, "all_reduce", lambda x, group=None: seen.append(group))
+
+    class Capped(_FakeCustom):
+        cap_bytes = 64  # 32 bf16
+
+        def can(self, x):
+            return 2 * x.numel() <= self.cap_bytes
+
+    fake = Capped(True)
+    x = torch.arange(96, dtype=torch.bfloat16)
+    TPGroup(group="pg", rank=0, size=2, custom=fake, chunk_large=True).all_reduce_(x)
+    assert fake.calls == 3 and not seen and torch.equal(x, 2 * torch.arange(96, dtype=torch.bfloat16))
+    TPGroup(group="pg", rank=0, size=2, custom=fake).all_reduce_(x)  # RCCL group: no chunking
+    assert fake.calls == 3 and seen == ["pg"]
+
+
 def _ref_sum(xs):
     acc = xs[0].float().clone()
     for x in xs[1:]:
@@ -137,18 +157,19 @@ def test_ipc_processes_one_gpu(tmp_path, world):
         assert res == {"ok": [True, True, True], "err": False}, (r, res)
 
 
-def _tp_worker(rank, world, port, out, back_to_back):
+def _tp_worker(rank, world, port, out, back_to_back, cap_mb):
     """The TP forward's collectives at Qwen3-32B / TP = 4 sizes, interleaved as in a forward:
     fused all-reduce + residual add + RMSNorm of a prefill chunk (1291 x 5120, 13 MB) and of a
     decode batch (8 x 5120), then the vocab-parallel logits gather (8 x 37984 per rank).
     back_to_back: no host sync between calls, and rank-dependent GEMM work before each call
-    (the ranks reach every collective at different times, as in a forward)."""
+    (the ranks reach every collective at different times, as in a forward).  cap_mb below the
+    prefill message: the group runs it through the kernels in pieces (chunk_large, gloo groups)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     import torch.distributed as dist
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    ar = CA.XGMIAllReduce(dist.group.WORLD, timeout_s=30.0)
-    tp = TPGroup(dist.group.WORLD, rank, world, custom=ar)
+    ar = CA.XGMIAllReduce(dist.group.WORLD, cap_bytes=cap_mb << 20, timeout_s=30.0)
+    tp = TPGroup(dist.group.WORLD, rank, world, custom=ar, chunk_large=True)
     H, V_local, errs, checks = 5120, 37984, [], []
     busy = torch.randn(4096 + 1024 * rank, 4096, device="cuda", dtype=torch.bfloat16)
     for it in range(2):
@@ -187,17 +208,17 @@ def _tp_worker(rank, world, port, out, back_to_back):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,back_to_back", [(2, False), (2, True), (4, False)])
-def test_ipc_tp_collectives_real_shapes(tmp_path, world, back_to_back):
+@pytest.mark.parametrize("world,back_to_back,cap_mb", [(2, False, 32), (2, True, 32), (4, False, 32), (2, False, 4)])
+def test_ipc_tp_collectives_real_shapes(tmp_path, world, back_to_back, cap_mb):
     """(4, True) is left out on purpose: 4 processes on ONE GPU are not all co-resident (the
     hardware time-slices the extra contexts), so a rank whose all-reduce kernel spins for a
     descheduled peer waits until its timeout (measured: the error word set, outputs wrong from
     the first late call on).  On a node each rank owns its GPU; this is a rehearsal limit."""
     out = str(tmp_path / "tpc")
-    mp.start_processes(_tp_worker, args=(world, _free_port(), out, back_to_back), nprocs=world, join=True,
+    mp.start_processes(_tp_worker, args=(world, _free_port(), out, back_to_back, cap_mb), nprocs=world, join=True,
                        start_method="spawn")
     for r in range(world):
         res = json.load(open(f"{out}.{r}"))
-        print(f"[tp-collectives] world={world} back_to_back={back_to_back} rank={r} {res}")
-        assert not res["err"] and res["calls"].get("3", 0) == 6, (r, res)
+        print(f"[tp-collectives] world={world} back_to_back={back_to_back} cap={cap_mb}MB rank={r} {res}")
+        assert not res["err"] and res["calls"].get("3", 0) == (6 if cap_mb >= 16 else 2 + 4 * 4), (r, res)
         assert max(res["errs"]) < 2e-2, (r, res)

@@ -2,14 +2,14 @@
 # Configs 4 and 5 at real shapes on ONE GPU (ranks share cuda:0; gloo + the xGMI all-reduce kernels
 # forced over IPC peer buffers): the real-shape TP numerics tests (TP = 4 on gloo collectives,
 # TP = 2 on the xGMI kernels), then the bench pool through the TP = 2 engine (driver/follower
-# plans, decode graphs with the all-reduce inside; BCG_AR_CAP_MB raised so that prefill chunks
-# also take the xGMI kernel instead of gloo host copies).  The plan-exchange cost is in
+# plans, decode graphs with the all-reduce inside; prefill chunks above the kernel cap
+# go through the xGMI kernels in pieces, not gloo host copies: TPGroup.chunk_large).  The plan-exchange cost is in
 # detail.phases_rank0 (plan_exchange).  Rehearsal only: the ranks time-share one GPU, so the
 # decisions/s here are not a measurement.  (TP = 4 engine runs need 4 co-resident ranks: only on
 # a node with one GPU per rank, see tests/test_tp_real_shapes_gpu.py.)
 set -o pipefail
 mkdir -p gpurun_out/tp
-export HSA_ENABLE_IPC_MODE_LEGACY=0 BCG_AR_CAP_MB=512
+export HSA_ENABLE_IPC_MODE_LEGACY=0
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 600 python -u -m pytest -x -v -rP --timeout 540 --timeout-method thread tests/test_tp_real_shapes_gpu.py \
     > gpurun_out/tp/tests.log 2>&1 || { tail -40 gpurun_out/tp/tests.log; exit 1; }
