@@ -96,6 +96,9 @@ class EngineArgs:
     admit_max_wait: int = 0
     admit_min_live: int = 64
     admit_min_tokens_frac: float = 1.5
+    # decode attention reads KV blocks shared by several rows (prefix cache) once per group
+    # of rows instead of once per row (engine/cascade.py); HIP backend only
+    cascade_decode: bool = True
 
     @classmethod
     def from_configs(cls, model: str, backend: str, weights: Optional[str] = None,
@@ -118,7 +121,8 @@ class EngineArgs:
                    overlap_prefill=ec.get("overlap_prefill", False),
                    precapture_graphs=ec.get("precapture_graphs", True),
                    kv_cache_dtype=ec.get("kv_cache_dtype", "auto"),
-                   admit_max_wait=int(ec.get("admit_max_wait", 0)))
+                   admit_max_wait=int(ec.get("admit_max_wait", 0)),
+                   cascade_decode=bool(ec.get("cascade_decode", True)))
         dtype = ec.get("dtype", "bfloat16")
         args.dtype = getattr(torch, dtype) if isinstance(dtype, str) else dtype
         for key, value in kw.items():
@@ -321,6 +325,11 @@ class InferenceEngine:
         # partial is written before it is read, so no initialisation is needed
         ws = self._decode_ws_bytes() // 4
         self.decode_ws = torch.empty(ws, dtype=torch.float32, device=dev) if ws else None
+        self.cascade = None
+        if self.backend == "hip" and self.args.cascade_decode and os.environ.get("BCG_CASCADE", "1") != "0":
+            from .cascade import CascadeTables
+            self.cascade = CascadeTables(cap, dev, self.args.kv_block_size)
+        self._layout_dirty = True  # live rows changed since the cascade tables were built
 
     def _phys(self, blocks: List[int]) -> List[int]:
         return [b + 1 for b in blocks]  # manager ids are shifted past scratch block 0
@@ -691,18 +700,33 @@ class InferenceEngine:
                 st[k].index_copy_(0, rows_d, v)
         for r in reqs:
             r.pending = False
+        self._layout_dirty = True
 
     def _decode_burst(self):
         """`poll_every` decode steps over the rows [0, bucket)."""
         rows = self._live_rows()
         n = rows[-1] + 1
+        if self.cascade is not None and self._layout_dirty:
+            self._regroup()
         with self.timer.phase("decode"):
             steps = self.graphs.run_burst(n) if self.graphs is not None else self._eager_burst(n)
         self.stats["decode_steps"] += steps
         self.stats["decode_row_steps"] += steps * len(rows)  # mean live rows = this / decode_steps
+        if self.cascade is not None:  # shared tokens read once per group instead of once per row
+            self.stats["cascade_shared_row_tokens"] = (self.stats.get("cascade_shared_row_tokens", 0)
+                                                       + steps * self.cascade.shared_row_blocks
+                                                       * self.args.kv_block_size)
         band = f"rows_le_{1 << max(0, (n - 1).bit_length()) if n <= 512 else (768 if n <= 768 else 1024 if n <= 1024 else 1536)}"
         self.stats[band] = self.stats.get(band, 0) + steps
         self._bursts += 1
+
+    def _regroup(self):
+        """Rebuild the shared-prefix tables from the live rows' block lists (engine/cascade.py)."""
+        from .cascade import plan_groups
+        with self.timer.phase("cascade_plan"):
+            rows = [(i, r.seq.blocks) for i, r in enumerate(self.slots) if r is not None and not r.pending]
+            self.cascade.upload(plan_groups(rows), self.model.n_q // self.model.n_kv)
+        self._layout_dirty = False
 
     def _eager_burst(self, n: int) -> int:
         view = {k: v[:n] for k, v in self.state.items()}
@@ -742,6 +766,7 @@ class InferenceEngine:
                 self.slots[i] = None
                 req.finish(text)
         self._park_rows(finished)
+        self._layout_dirty = True
         self._compact()
 
     def _park_rows(self, rows: List[int]):
@@ -880,7 +905,7 @@ class InferenceEngine:
         rows = torch.arange(pos.shape[0], device=pos.device)
         slots = st["block_tables"][rows, (pos // bs).long()] * bs + pos % bs
         return AttnMeta(positions=pos, slots=slots.to(torch.int32), block_tables=st["block_tables"],
-                        seq_lens=st["seq_lens"], decode=True, workspace=self.decode_ws)
+                        seq_lens=st["seq_lens"], decode=True, workspace=self.decode_ws, cascade=self.cascade)
 
     def decode_step(self, st: Dict[str, torch.Tensor]):
         """One full decode step (forward + guided sampling), graph-capturable."""

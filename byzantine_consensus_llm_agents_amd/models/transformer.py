@@ -39,6 +39,7 @@ class AttnMeta:
     logits_idx: Optional[torch.Tensor] = None  # rows whose logits are needed
     tiles: Optional[torch.Tensor] = None       # [n_tiles, 3] int32 prefill work list (HIP kernel)
     workspace: Optional[torch.Tensor] = None   # decode split-K scratch shared by all graphs (HIP)
+    cascade: Optional[object] = None           # decode shared-prefix tables (engine/cascade.py)
 
 
 class TPGroup:
@@ -308,7 +309,7 @@ class DecoderModel:
                                       k_cache, v_cache, li)
         if meta.decode:
             return ops.paged_attention_decode(q, k_cache, v_cache, li, meta.block_tables, meta.seq_lens,
-                                              self.scale, meta.workspace)
+                                              self.scale, meta.workspace, meta.cascade)
         return ops.paged_attention_prefill(q, k_cache, v_cache, li, meta.block_tables, meta.q_start,
                                            meta.seq_lens, self.scale, meta.max_q_len, meta.tiles)
 

@@ -13,7 +13,8 @@ from . import reference as _ref
 
 
 def _torch_ops() -> SimpleNamespace:
-    def decode(q, k_cache, v_cache, layer, block_tables, seq_lens, scale, workspace=None):
+    def decode(q, k_cache, v_cache, layer, block_tables, seq_lens, scale, workspace=None, cascade=None):
+        # the shared-prefix cascade changes how the kernel walks the KV, not the result
         B = q.shape[0]
         q_start = torch.arange(B + 1, dtype=torch.int32, device=q.device)
         return _ref.paged_attention(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale)

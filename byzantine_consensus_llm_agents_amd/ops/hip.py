@@ -38,11 +38,13 @@ def load_library(path: str = None) -> ctypes.CDLL:
                                       c_float, c_int, c_void_p],
         "bcg_paged_attention_decode": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                        c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int,
-                                       c_int, c_void_p, c_int, c_void_p],
+                                       c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                       c_int, c_void_p, c_void_p, c_int, c_int, c_void_p],
         "bcg_paged_attention_prefill": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                                         c_void_p, c_int, c_int, c_void_p],
         "bcg_decode_split_tokens": [c_int, c_int, c_int],
+        "bcg_decode_max_splits": [c_int],
         "bcg_quant_fp8": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
         "bcg_add_rmsnorm_fp8": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_int,
                                 c_void_p],
@@ -154,14 +156,17 @@ def hip_ops() -> SimpleNamespace:
         return q
 
     def decode_workspace_numel(B, n_q, hd, max_blocks, block_size=16):
-        """fp32 split partials (o, m, l) of the flash-decoding split-K."""
-        split = lib.bcg_decode_split_tokens(B, 0, max_blocks * block_size)
-        max_splits = (max_blocks * block_size + split - 1) // split
+        """fp32 split partials (o, m, l) of the flash-decoding split-K (+ slot 0 of the
+        shared-prefix pass)."""
+        max_splits = lib.bcg_decode_max_splits(max_blocks * block_size)
         return B * n_q * max_splits * (hd + 2)
 
-    def paged_attention_decode(q, k_cache, v_cache, layer, block_tables, seq_lens, scale, workspace=None):
+    def paged_attention_decode(q, k_cache, v_cache, layer, block_tables, seq_lens, scale, workspace=None,
+                               cascade=None):
         """`workspace`: optional fp32 split-K scratch of >= decode_workspace_numel(...) elements,
-        shared by every decode graph (it is dead between launches) instead of one per graph."""
+        shared by every decode graph (it is dead between launches) instead of one per graph.
+        `cascade`: optional shared-prefix tables (``engine/cascade.py`` ``CascadeTables``):
+        rows whose leading KV blocks are shared read them once per group."""
         B, n_q, hd = q.shape
         L, NB, n_kv, BS, _ = k_cache.shape
         _req(q.is_contiguous() and block_tables.dtype == torch.int32 and block_tables.is_contiguous()
@@ -169,7 +174,7 @@ def hip_ops() -> SimpleNamespace:
         max_blocks = block_tables.shape[1]
         _req(B <= 2048, "decode attention: at most 2048 rows")
         split = lib.bcg_decode_split_tokens(B, n_kv, max_blocks * BS)
-        max_splits = (max_blocks * BS + split - 1) // split
+        max_splits = lib.bcg_decode_max_splits(max_blocks * BS)
         need = B * n_q * max_splits * (hd + 2)
         if workspace is None:
             ws = torch.empty(need, dtype=torch.float32, device=q.device)
@@ -177,11 +182,22 @@ def hip_ops() -> SimpleNamespace:
             _req(workspace.dtype == torch.float32 and workspace.is_contiguous() and workspace.numel() >= need,
                  "decode attention workspace too small")
             ws = workspace
+        cas = [None, None, None, 0, None, 0, None, None, 0, 32]
+        if cascade is not None:
+            c = cascade
+            i32 = torch.int32
+            for t in (c.kv_begin, c.split_base, c.grp_rows, c.grp_desc, c.items, c.n_items):
+                _req(t.dtype == i32 and t.is_contiguous() and t.device == q.device, "cascade tables: int32 on device")
+            _req(c.kv_begin.numel() >= B and c.split_base.numel() >= B, "cascade tables: one entry per row")
+            _req(c.grp_desc.dim() == 2 and c.grp_desc.shape[1] == 4 and c.items.dim() == 2 and c.items.shape[1] == 4
+                 and c.n_items.numel() >= 1, "cascade tables: grp_desc [G, 4], items [I, 4], n_items [1]")
+            cas = [_p(c.kv_begin), _p(c.split_base), _p(c.grp_rows), c.grp_rows.numel(), _p(c.grp_desc),
+                   c.grp_desc.shape[0], _p(c.items), _p(c.n_items), c.items.shape[0], c.split_tokens]
         out = torch.empty(B, n_q * hd, dtype=q.dtype, device=q.device)
         _check(lib.bcg_paged_attention_decode(
             _p(q), _p(k_cache), _p(v_cache), layer, NB, n_kv, _p(block_tables), max_blocks, _p(seq_lens),
-            B, n_q, hd, BS, scale, _p(ws), max_splits, split, _p(out), _kv_fp8(k_cache, v_cache), _stream()),
-            "paged_attention_decode")
+            B, n_q, hd, BS, scale, _p(ws), max_splits, split, _p(out), _kv_fp8(k_cache, v_cache), *cas,
+            _stream()), "paged_attention_decode")
         return out
 
     def paged_attention_prefill(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale,

@@ -129,6 +129,56 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     return out.reshape(T, n_q * hd).to(q.dtype)
 
 
+def _partial(q, k, v, scale):
+    """(O unnormalised, m, l) of q [n_q, hd] over k, v [n_q, n, hd] -- one flash-decoding split."""
+    s = torch.einsum("hd,hnd->hn", q, k) * scale
+    m = s.max(-1).values
+    p = torch.exp(s - m[:, None])
+    return torch.einsum("hn,hnd->hd", p, v), m, p.sum(-1)
+
+
+def paged_attention_decode_cascade(q, k_cache, v_cache, layer, block_tables, seq_lens, scale, cascade):
+    """Decode attention the way the HIP cascade computes it, from its tables (fp32).
+
+    A grouped row's tokens [0, kv_begin) come from its group's FIRST member's block table
+    (``decode_shared_kernel``, in pieces -- merged here as one); [kv_begin, ctx) from its own
+    (``decode_attn_kernel``); the partials merge as flash-decoding splits do.  Equal to
+    `paged_attention` exactly when the tables are consistent (every member holds the group's
+    block ids) -- what the CPU tests of ``engine/cascade.py`` check.  ``cascade``: CascadeTables (any device)."""
+    B, n_q, hd = q.shape
+    n_kv = k_cache.shape[2]
+    group = n_q // n_kv
+    kv_begin = cascade.kv_begin.cpu().tolist()
+    lead_of = {}
+    desc = cascade.grp_desc.cpu().tolist()
+    rows = cascade.grp_rows.cpu().tolist()
+    items = cascade.items.cpu().tolist()[:int(cascade.n_items[0])]
+    for g, _, _, _ in items:
+        first, n, shared = desc[g][:3]
+        for m in rows[first:first + n]:
+            lead_of[m] = (rows[first], shared * k_cache.shape[3])
+    out = torch.zeros(B, n_q, hd, dtype=torch.float32)
+    for b in range(B):
+        ctx = int(seq_lens[b])
+        qb = q[b].float().cpu()
+        parts = []
+        begin = kv_begin[b]
+        if begin:
+            lead, shared = lead_of[b]
+            assert shared == begin, "kv_begin disagrees with the group table"
+            k = _gather_kv(k_cache, layer, block_tables[lead], shared).float().cpu().repeat_interleave(group, 0)
+            v = _gather_kv(v_cache, layer, block_tables[lead], shared, True).float().cpu().repeat_interleave(group, 0)
+            parts.append(_partial(qb, k, v, scale))
+        k = _gather_kv(k_cache, layer, block_tables[b], ctx).float().cpu()[:, begin:].repeat_interleave(group, 0)
+        v = _gather_kv(v_cache, layer, block_tables[b], ctx, True).float().cpu()[:, begin:].repeat_interleave(group, 0)
+        parts.append(_partial(qb, k, v, scale))
+        m = torch.stack([p[1] for p in parts]).max(0).values
+        o = sum(p[0] * torch.exp(p[1] - m)[:, None] for p in parts)
+        l_sum = sum(p[2] * torch.exp(p[1] - m) for p in parts)
+        out[b] = o / l_sum[:, None]
+    return out.reshape(B, n_q * hd).to(q.dtype)
+
+
 def linear_silu(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """silu(x Wg^T) * (x Wu^T) with W = [gate; up]: the fused gate_up GEMM epilogue (fp32 math)."""
     gu = x.float() @ w.float().t()

@@ -351,11 +351,21 @@ struct Causal {
 // B = 160, ctx 1700, max_model_len 8192.
 constexpr int DEC_MAX_B = 2048;
 
+//
+// Shared-prefix (cascade) form: rows whose leading blocks are the SAME physical blocks
+// (prefix cache: an agent's system prompt, identical in every game) get kv_begin[b] =
+// the shared token count and split_base[b] = the shared pass's split count.
+// decode_shared_kernel computes their attention over the shared blocks once per group --
+// every member's query heads packed into MFMA columns, each shared K/V byte read once per
+// 64 columns instead of once per row -- into slots 0 .. split_base-1; this kernel covers
+// [kv_begin, ctx) into the slots after them; the combine merges all slots.
+// kv_begin == nullptr: no cascade (every row from token 0).
 template <int HD, bool F8 = false, int CPW = 1>
 __global__ __launch_bounds__(256) void decode_attn_kernel(
     const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
     const int* __restrict__ seq_lens, int B, int n_q, float scale_log2, float* __restrict__ part_o,
-    float* __restrict__ part_ml, int max_splits) {
+    float* __restrict__ part_ml, int max_splits, const int* __restrict__ kv_begin,
+    const int* __restrict__ split_base) {
   // CPW chunks per wave: an item covers DEC_WAVES * CPW * 32 tokens; every chunk's loads of
   // a wave are issued before its first MFMA (CPW x 16 loads in flight per wave), and the
   // split partials / merge traffic shrink by CPW
@@ -376,7 +386,8 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
 #pragma unroll
     for (int j = 0; j < PER_MAX; ++j) {
       const int i = tid * per + j;
-      cnt[j] = (j < per && i < B) ? (seq_lens[i] + DEC_SPLIT - 1) / DEC_SPLIT : 0;
+      const int own = (j < per && i < B) ? max(0, seq_lens[i] - (kv_begin ? kv_begin[i] : 0)) : 0;
+      cnt[j] = (own + DEC_SPLIT - 1) / DEC_SPLIT;
       sum += cnt[j];
     }
     int incl = sum;  // inclusive wave scan
@@ -409,7 +420,8 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
     }
     const int b = lo, split = pos - s_pre[b];
     const int ctx = seq_lens[b];
-    const int start = split * DEC_SPLIT;
+    const int start = (kv_begin ? kv_begin[b] : 0) + split * DEC_SPLIT;
+    const int slot = (split_base ? split_base[b] : 0) + split;  // after the shared-pass slots
     const int* table = block_tables + static_cast<size_t>(b) * max_blocks;
 
     bf16x8 bq[HD / 32];
@@ -461,7 +473,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
         ll += s_ml[ww][1][qi] * f;
         oo += s_o[ww][d][qi] * f;
       }
-      const size_t pidx = (static_cast<size_t>(b) * n_q + kvh * G + qi) * max_splits + split;
+      const size_t pidx = (static_cast<size_t>(b) * n_q + kvh * G + qi) * max_splits + slot;
       part_o[pidx * HD + d] = oo;
       if (d == 0) {
         part_ml[pidx * 2] = mm;
@@ -481,13 +493,16 @@ constexpr int COMBINE_WAVES = 4;
 template <int HD>
 __global__ __launch_bounds__(64 * COMBINE_WAVES) void decode_combine_kernel(
     const float* __restrict__ part_o, const float* __restrict__ part_ml, const int* __restrict__ seq_lens, int n_q,
-    int max_splits, int split_tokens, int n_bq, bf16_t* __restrict__ out) {
+    int max_splits, int split_tokens, int n_bq, bf16_t* __restrict__ out, const int* __restrict__ kv_begin,
+    const int* __restrict__ split_base) {
   constexpr int PER = HD / 64;  // dims per lane
   const int lane = threadIdx.x & 63;
   const int bq = blockIdx.x * COMBINE_WAVES + (threadIdx.x >> 6);
   if (bq >= n_bq) return;  // wave-uniform
   const int b = bq / n_q;
-  const int ns = (seq_lens[b] + split_tokens - 1) / split_tokens;  // <= max_splits <= 64 (host check)
+  const int own = max(0, seq_lens[b] - (kv_begin ? kv_begin[b] : 0));
+  // <= max_splits <= 64 (host check); slots 0 .. split_base[b]-1 hold the shared-prefix partials
+  const int ns = (split_base ? split_base[b] : 0) + (own + split_tokens - 1) / split_tokens;
   const float2 mlv = lane < ns ? reinterpret_cast<const float2*>(part_ml)[static_cast<size_t>(bq) * max_splits + lane]
                                : float2{-INFINITY, 0.f};
   float mm = mlv.x;
@@ -525,12 +540,145 @@ __global__ __launch_bounds__(64 * COMBINE_WAVES) void decode_combine_kernel(
   for (int e = 0; e < PER; ++e) out[static_cast<size_t>(bq) * HD + lane * PER + e] = f2bf(acc[e] * inv);
 }
 
+// ------------------------------------------------------- decode, shared prefix
+// Work item (one wave) = (group, 64-column block, shared split) for the kv head blockIdx.y.  A group's
+// columns are its (member, query head) pairs, c = member * G + head, 16 per MFMA tile and
+// SH_NT tiles per wave, so the G = n_q / n_kv heads of up to 64 / G rows share every
+// 16-B K/V load (the per-row kernel packs only one row's G heads into the 16 columns).
+// grp_desc[grp] = {first member in grp_rows, members, shared blocks, unused}; the shared
+// block ids are read from the first member's table row (every member holds the same ids
+// there).  The shared tokens are all visible to every member (they precede each member's
+// own tokens), so the loop is the prefill kernel's full-visibility block (K/V reloaded in
+// place, lazy rescale outside the inner loop) plus one masked half chunk for an odd block
+// count.  Splitting the shared tokens into split_tokens pieces (own slots) keeps each wave's
+// dependent chunk chain short: one whole-prefix item per wave was latency-bound (a 640-token
+// prefix = 20 chained chunk loads) and left most SIMDs idle.  Out: slot `split` of each
+// member's (m, l, O) partials.  Every table entry is
+// range-checked before use: a bad item is skipped, never dereferenced.
+constexpr int SH_NT = 4;
+constexpr int SH_WAVES = 4;
+
+template <int HD, bool F8>
+__global__ __launch_bounds__(64 * SH_WAVES) void decode_shared_kernel(
+    const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks, int B, int n_q,
+    float scale_log2, const int* __restrict__ grp_rows, int grp_cap, const int* __restrict__ grp_desc,
+    int max_groups, const int* __restrict__ items, const int* __restrict__ n_items_p, int max_items,
+    int split_tokens, float* __restrict__ part_o, float* __restrict__ part_ml, int max_splits) {
+  constexpr int NT = SH_NT;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 15, h = lane >> 4;
+  const int kvh = blockIdx.y;
+  const int G = n_q / g.n_kv;
+  const int n_items = min(*n_items_p, max_items);
+  for (int it = blockIdx.x * SH_WAVES + w; it < n_items; it += gridDim.x * SH_WAVES) {
+    const int grp = items[4 * it], cb = items[4 * it + 1], sp = items[4 * it + 2];
+    if (grp < 0 || grp >= max_groups || cb < 0 || sp < 0 || sp >= max_splits) continue;  // wave-uniform
+    const int mbeg = grp_desc[4 * grp], nmem = grp_desc[4 * grp + 1], nblk = grp_desc[4 * grp + 2];
+    if (mbeg < 0 || nmem <= 0 || mbeg + nmem > grp_cap || nblk <= 0 || nblk > max_blocks) continue;
+    const int lead = grp_rows[mbeg];
+    if (lead < 0 || lead >= B) continue;
+    const int* table = block_tables + static_cast<size_t>(lead) * max_blocks;
+    const int S = nblk * BS;
+    const int t_lo = sp * split_tokens, t_hi = min(S, t_lo + split_tokens);  // this item's shared tokens
+    if (t_lo >= S) continue;
+    const int ncol = nmem * G;
+
+    bf16x8 bq[NT][HD / 32];
+    int qrow[NT], qhd[NT];  // this lane's column: row and query head (qrow < 0: no column)
+    float m[NT], l[NT];
+    f32x4 o[NT][HD / 16];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int col = cb * (16 * NT) + nt * 16 + r;
+      const int mem = col / G;
+      int row = col < ncol ? grp_rows[mbeg + mem] : -1;
+      if (row >= B) row = -1;
+      const int hq = kvh * G + (col - mem * G);
+      load_q<HD>(bq[nt], q + (static_cast<size_t>(row >= 0 ? row : 0) * n_q + (row >= 0 ? hq : 0)) * HD, row >= 0,
+                 lane);
+      qrow[nt] = row;
+      qhd[nt] = hq;
+      m[nt] = -INFINITY;
+      l[nt] = 0.f;
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) o[nt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+
+    // absolute chunk indices; split_tokens is a multiple of CHUNK, so only the group's last
+    // split can end in a half chunk (odd block count)
+    const int nchunk = (t_hi + CHUNK - 1) / CHUNK, n_full = t_hi / CHUNK;
+    int c = t_lo / CHUNK;
+    Chunk<HD, F8> cur;
+    load_chunk<HD, F8>(cur, g, table[2 * c], table[min(2 * c + 1, nblk - 1)], kvh, lane);
+    while (c < n_full) {
+      f32x4 s[NT][2];
+      float mx[NT];
+      bool grow = false;
+      int b0 = 0, b1 = 0;
+      for (; c < n_full; ++c) {
+        const int cn = min(c + 1, nchunk - 1);
+        b0 = table[2 * cn], b1 = table[min(2 * cn + 1, nblk - 1)];
+        grow = full_scores<HD, NT, F8>(cur, bq, scale_log2, m, s, mx,
+                                       [&](Chunk<HD, F8>& x) { load_chunk_k<HD, F8>(x, g, b0, b1, kvh, lane); });
+        if (grow) break;  // wave-uniform
+        full_pv<HD, NT, F8>(cur, s, scale_log2, m, l, o,
+                            [&](Chunk<HD, F8>& x) { load_chunk_v<HD, F8>(x, g, b0, b1, kvh, lane); });
+      }
+      if (!grow) break;
+      full_rescale<HD, NT>(mx, m, l, o);
+      full_pv<HD, NT, F8>(cur, s, scale_log2, m, l, o,
+                          [&](Chunk<HD, F8>& x) { load_chunk_v<HD, F8>(x, g, b0, b1, kvh, lane); });
+      ++c;
+    }
+    if (c < nchunk) {  // odd block count: the last 16 tokens, masked at S (cur holds that chunk)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        compute_chunk<HD, AllVisible, true, F8>(cur, bq[nt], c * CHUNK, t_hi, AllVisible{}, scale_log2, m[nt],
+                                                l[nt], o[nt], lane);
+    }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      if (qrow[nt] < 0) continue;
+      const size_t pidx = (static_cast<size_t>(qrow[nt]) * n_q + qhd[nt]) * max_splits + sp;
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt)
+        *reinterpret_cast<f32x4*>(part_o + pidx * HD + dt * 16 + 4 * h) = o[nt][dt];
+      if (h == 0) {
+        part_ml[pidx * 2] = m[nt];
+        part_ml[pidx * 2 + 1] = l[nt];
+      }
+    }
+  }
+}
+
+struct Cascade {
+  const int* kv_begin;    // [B] shared tokens per row (0: none)
+  const int* split_base;  // [B] shared-pass splits of the row (its partial slots 0 .. split_base-1)
+  const int* grp_rows;    // [grp_cap] members, grouped
+  int grp_cap;
+  const int* grp_desc;    // [max_groups, 4]
+  int max_groups;
+  const int* items;       // [max_items, 4] (group, 64-column block, shared split, -)
+  const int* n_items;     // [1] live items (device: graph replays see the current count)
+  int max_items;
+  int split_tokens;       // shared tokens per item (a multiple of CHUNK)
+};
+
 template <int HD, bool F8 = false, int CPW = 1>
 void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks, const int* seq_lens, int B,
-                   int n_q, float sl, float* ws, int max_splits, bf16_t* out, hipStream_t stream) {
+                   int n_q, float sl, float* ws, int max_splits, bf16_t* out, const Cascade& cas,
+                   hipStream_t stream) {
   constexpr int DEC_SPLIT = DEC_WAVES * CHUNK * CPW;
   float* part_o = ws;
   float* part_ml = ws + static_cast<size_t>(B) * n_q * max_splits * HD;
+  if (cas.kv_begin != nullptr && cas.max_items > 0) {
+    // grid fixed by the item capacity (graph-safe); the live count is read on the device
+    const int per_kv = std::max(1, std::min((cas.max_items + SH_WAVES - 1) / SH_WAVES, 128));
+    hipLaunchKernelGGL((decode_shared_kernel<HD, F8>), dim3(per_kv, g.n_kv), dim3(64 * SH_WAVES), 0, stream, q, g,
+                       tables, max_blocks, B, n_q, sl, cas.grp_rows, cas.grp_cap, cas.grp_desc, cas.max_groups,
+                       cas.items, cas.n_items, cas.max_items, cas.split_tokens, part_o, part_ml, max_splits);
+  }
   // fixed (graph-safe) grid striding over the live items: one full wave of resident workgroups
   static int resident = 0;
   if (resident == 0) {
@@ -542,11 +690,11 @@ void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
   }
   const int grid = static_cast<int>(std::min<long>(static_cast<long>(B) * g.n_kv * max_splits, resident));
   hipLaunchKernelGGL((decode_attn_kernel<HD, F8, CPW>), dim3(grid), dim3(256), 0, stream, q, g, tables, max_blocks,
-                     seq_lens, B, n_q, sl, part_o, part_ml, max_splits);
+                     seq_lens, B, n_q, sl, part_o, part_ml, max_splits, cas.kv_begin, cas.split_base);
   const int n_bq = B * n_q;
   hipLaunchKernelGGL(decode_combine_kernel<HD>, dim3((n_bq + COMBINE_WAVES - 1) / COMBINE_WAVES),
                      dim3(64 * COMBINE_WAVES), 0, stream, part_o, part_ml, seq_lens, n_q, max_splits, DEC_SPLIT, n_bq,
-                     out);
+                     out, cas.kv_begin, cas.split_base);
 }
 
 // ----------------------------------------------------------------- prefill
@@ -712,32 +860,51 @@ void launch_prefill(int n_tiles, int n_q, const bf16_t* q, KVGeom g, const int* 
 // merge kernel reads.  (Looping a wave over chunks one at a time was slower: 2-2.6 TB/s.)
 constexpr int DEC_CPW = 2;
 BCG_API int bcg_decode_split_tokens(int B, int n_kv, int max_tokens) { return DEC_WAVES * CHUNK * DEC_CPW; }
+// Partial slots per (row, head): a row's own splits + up to DEC_MAX_SHARED_SPLITS of the
+// shared-prefix pass (engine/cascade.py keeps shared tokens / its split within it).
+constexpr int DEC_MAX_SHARED_SPLITS = 16;
+BCG_API int bcg_decode_max_splits(int max_tokens) {
+  const int split = DEC_WAVES * CHUNK * DEC_CPW;
+  return (max_tokens + split - 1) / split + DEC_MAX_SHARED_SPLITS;
+}
 
 // kv_fp8: the caches hold OCP e4m3fn bytes (scale 1) instead of bf16.
 BCG_API int bcg_paged_attention_decode(const void* q, const void* k_cache, const void* v_cache, int layer,
                                        int num_blocks, int n_kv, const int* block_tables, int max_blocks,
                                        const int* seq_lens, int B, int n_q, int hd, int block_size,
                                        float scale, float* workspace, int max_splits, int split_tokens,
-                                       void* out, int kv_fp8, hipStream_t stream) {
+                                       void* out, int kv_fp8, const int* kv_begin, const int* split_base,
+                                       const int* grp_rows, int grp_cap, const int* grp_desc, int max_groups,
+                                       const int* items, const int* n_items, int max_items,
+                                       int shared_split_tokens, hipStream_t stream) {
   if (block_size != BS || n_q % n_kv || n_q / n_kv > 16 || B <= 0 || B > DEC_MAX_B) return -2;
-  if (split_tokens != DEC_WAVES * CHUNK * DEC_CPW || max_splits * split_tokens < max_blocks * BS) return -3;
+  // with the cascade a row's own splits start after its shared tokens, in the slots after the
+  // shared splits: the host sizes max_splits for both (bcg_decode_max_splits)
+  const int own_slots = max_splits - (kv_begin ? DEC_MAX_SHARED_SPLITS : 0);
+  if (split_tokens != DEC_WAVES * CHUNK * DEC_CPW || own_slots * split_tokens < max_blocks * BS) return -3;
   if (max_splits > 64) return -3;  // decode_combine_kernel: one lane per split
+  Cascade cas{kv_begin, split_base, grp_rows, grp_cap, grp_desc, max_groups, items, n_items, max_items,
+              shared_split_tokens};
+  if (kv_begin && (!split_base || !grp_rows || !grp_desc || !items || !n_items || grp_cap < 0 || max_groups < 0 ||
+                   max_items < 0 || shared_split_tokens <= 0 || shared_split_tokens % CHUNK))
+    return -4;
+  if (!kv_begin) cas = Cascade{nullptr, nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr, 0, CHUNK};
   KVGeom g{static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), layer, num_blocks, n_kv};
   const bf16_t* qb = static_cast<const bf16_t*>(q);
   bf16_t* ob = static_cast<bf16_t*>(out);
   const float sl = scale * LOG2E;
   if (hd == 128 && kv_fp8) {
     launch_decode<128, true, DEC_CPW>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace,
-                                             max_splits, ob, stream);
+                                             max_splits, ob, cas, stream);
   } else if (hd == 128) {
     launch_decode<128, false, DEC_CPW>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace,
-                                              max_splits, ob, stream);
+                                              max_splits, ob, cas, stream);
   } else if (hd == 64 && kv_fp8) {
     launch_decode<64, true, DEC_CPW>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace,
-                                            max_splits, ob, stream);
+                                            max_splits, ob, cas, stream);
   } else if (hd == 64) {
     launch_decode<64, false, DEC_CPW>(qb, g, block_tables, max_blocks, seq_lens, B, n_q, sl, workspace,
-                                             max_splits, ob, stream);
+                                             max_splits, ob, cas, stream);
   } else {
     return -2;
   }
