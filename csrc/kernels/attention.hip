@@ -712,6 +712,9 @@ void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
 #ifndef PREFILL_FULL_BLOCK
 #define PREFILL_FULL_BLOCK 1  // fully visible chunks through full_scores / full_pv (lazy rescale outside the inner loop, in-place reload)
 #endif
+#ifndef PREFILL_XCD_ORDER
+#define PREFILL_XCD_ORDER 0  // default grid order (BCG_PREFILL_XCD_ORDER=0/1 overrides at run time)
+#endif
 #ifndef PREFILL_WPE
 #define PREFILL_WPE 0
 #endif
@@ -724,12 +727,25 @@ template <int HD, int NT, bool F8 = false>
 __global__ __launch_bounds__(256) PREFILL_ATTR void prefill_attn_kernel(
     const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
     const int* __restrict__ q_start, const int* __restrict__ seq_lens, const int* __restrict__ tiles,
-    int n_q, float scale_log2, bf16_t* __restrict__ out) {
+    int n_q, float scale_log2, bf16_t* __restrict__ out, int n_tiles, int xcd_order) {
   constexpr int RG = 4 / NT;   // row groups per 64-row tile
   constexpr int ROWS = 16 * NT;
-  const int tile = blockIdx.x;
+  // xcd_order: 1-D grid; workgroup id b runs on XCD b % 8 (round-robin dispatch), so the
+  // head groups of one tile are given consecutive ids of ONE XCD -- the query heads that share
+  // a kv head then read its K/V through that XCD's L2 together -- while each XCD still walks
+  // the tiles in the host's deepest-first order (tile = 8 * local index + XCD).
+  int tile, hgrp;
+  if (xcd_order) {
+    const int hg_n = (n_q + NT - 1) / NT, s = blockIdx.x >> 3;
+    tile = (s / hg_n) * 8 + (blockIdx.x & 7);
+    hgrp = s % hg_n;
+    if (tile >= n_tiles) return;  // padding of the grid to whole XCD rounds
+  } else {
+    tile = blockIdx.x;
+    hgrp = blockIdx.y;
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int qh = blockIdx.y * NT + w / RG;
+  const int qh = hgrp * NT + w / RG;
   if (qh >= n_q) return;  // wave-uniform; no block-level barriers in this kernel
   const int b = tiles[3 * tile], q_begin = tiles[3 * tile + 1], q_end = tiles[3 * tile + 2];
   const int r = lane & 15, h = lane >> 4;
@@ -847,8 +863,19 @@ void launch_prefill(int n_tiles, int n_q, const bf16_t* q, KVGeom g, const int* 
                     const int* q_start, const int* seq_lens, const int* tiles, float sl, bf16_t* out,
                     hipStream_t stream) {
   constexpr int NT = 4;  // 1 and 2 measured slower (PERF.md); the LDS-shared forms were 180-200 TF/s
-  hipLaunchKernelGGL((prefill_attn_kernel<HD, NT, F8>), dim3(n_tiles, (n_q + NT - 1) / NT), dim3(256), 0, stream, q,
-                     g, tables, max_blocks, q_start, seq_lens, tiles, n_q, sl, out);
+  const int hg_n = (n_q + NT - 1) / NT;
+  static const int xcd_order = [] {
+    const char* e = std::getenv("BCG_PREFILL_XCD_ORDER");
+    return e ? std::atoi(e) : PREFILL_XCD_ORDER;
+  }();
+  if (xcd_order) {
+    const int rounds = (n_tiles + 7) / 8;
+    hipLaunchKernelGGL((prefill_attn_kernel<HD, NT, F8>), dim3(rounds * 8 * hg_n), dim3(256), 0, stream, q, g,
+                       tables, max_blocks, q_start, seq_lens, tiles, n_q, sl, out, n_tiles, 1);
+  } else {
+    hipLaunchKernelGGL((prefill_attn_kernel<HD, NT, F8>), dim3(n_tiles, hg_n), dim3(256), 0, stream, q, g, tables,
+                       max_blocks, q_start, seq_lens, tiles, n_q, sl, out, n_tiles, 0);
+  }
 }
 
 }  // namespace

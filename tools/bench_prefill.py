@@ -68,6 +68,7 @@ def attention(cfg, n_prompts, prompt, prefix):
     for i in range(n_prompts):
         for t in range(i * prompt, (i + 1) * prompt, 64):
             tiles.append((i, t, min(t + 64, (i + 1) * prompt)))
+    tiles.sort(key=lambda x: -(x[2] - x[0] * prompt))  # deepest first, as the engine orders them
     tiles = torch.tensor(tiles, dtype=torch.int32).cuda()
     T = n_prompts * prompt
     q = torch.randn(T, n_q, hd, device="cuda", dtype=torch.bfloat16)
