@@ -31,8 +31,9 @@ def test_add_rmsnorm(hip, H, has_res):
     _close(y, y_ref, atol=2e-2)
 
 
-def test_silu_mul(hip):
-    gu = torch.randn(19, 2 * 17408, device="cuda", dtype=torch.bfloat16)
+@pytest.mark.parametrize("T", [19, 5003])
+def test_silu_mul(hip, T):
+    gu = torch.randn(T, 2 * 17408, device="cuda", dtype=torch.bfloat16)
     _close(hip.silu_mul(gu), R.silu_mul(gu), atol=2e-2)
 
 
