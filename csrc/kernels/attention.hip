@@ -44,6 +44,21 @@ constexpr float RESCALE_LOG2 = 8.f;  // lazy online-softmax rescale threshold (l
 // arguments are <= 0 here and a result below 2^-126 may flush to 0.
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// Single-instruction maxima.  fmaxf() on MFMA results makes hipcc canonicalise every input
+// first (one v_max_f32 x, x per score: 32 extra VALU per 64 MFMAs in the prefill loop); the
+// scores here are never NaN, so the raw v_max3 / v_max forms are exact.
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float vmax(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 struct KVGeom {
   const bf16_t* k;   // [L, NB, n_kv, BS, HD]
   const bf16_t* v;   // [L, NB, n_kv, HD, BS]
@@ -142,9 +157,9 @@ __device__ __forceinline__ void load_chunk_v(Chunk<HD, F8>& c, const KVGeom& g, 
 // halves of each swap are combined, so every lane gets identical bits.
 __device__ __forceinline__ float rows_max(float v) {
   const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  v = vmax(__uint_as_float(a[0]), __uint_as_float(a[1]));
   const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+  return vmax(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 
 __device__ __forceinline__ float rows_sum(float v) {
@@ -258,8 +273,9 @@ __device__ __forceinline__ void compute_chunk(const Chunk<HD, F8>& c, const bf16
 // v_accvgpr_read per 64 MFMAs at NT = 4); outside it, O stays in AGPRs.
 template <int HD, int NT, bool F8, typename ReloadK>
 __device__ __forceinline__ bool full_scores(Chunk<HD, F8>& c, const bf16x8 (&bq)[NT][HD / 32], float scale_log2,
-                                            const float (&m)[NT], f32x4 (&s)[NT][2], float (&mx)[NT],
+                                            const float (&m)[NT], f32x2 (&t)[NT][4], float (&mx)[NT],
                                             ReloadK reload_k) {
+  f32x4 s[NT][2];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -270,32 +286,42 @@ __device__ __forceinline__ bool full_scores(Chunk<HD, F8>& c, const bf16x8 (&bq)
         s[nt][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(to_bf16x8(c.k[u][kk]), bq[nt][kk], s[nt][u], 0, 0, 0);
     }
   reload_k(c);  // next chunk's K into the registers the S^T MFMAs just read
+  // every score is read from the MFMA result ONCE: t = S * scale - m (two per v_pk_fma_f32), its
+  // column max decides the lazy rescale, and full_pv exponentiates t directly
+  // (before the first chunk m = -inf: t is taken relative to 0 and the chunk always rescales)
   bool grow = false;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
-    float v = fmaxf(fmaxf(fmaxf(s[nt][0][0], s[nt][0][1]), fmaxf(s[nt][0][2], s[nt][0][3])),
-                    fmaxf(fmaxf(s[nt][1][0], s[nt][1][1]), fmaxf(s[nt][1][2], s[nt][1][3])));
-    mx[nt] = rows_max(v * scale_log2);
-    grow |= mx[nt] > m[nt] + RESCALE_LOG2;
+    const bool first = m[nt] == -INFINITY;
+    const float m_eff = first ? 0.f : m[nt];
+    const f32x2 sc = {scale_log2, scale_log2}, mm = {m_eff, m_eff};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      t[nt][q] = f32x2{s[nt][q >> 1][2 * (q & 1)], s[nt][q >> 1][2 * (q & 1) + 1]} * sc - mm;
+    const float v = vmax3(vmax3(t[nt][0].x, t[nt][0].y, t[nt][1].x), vmax3(t[nt][1].y, t[nt][2].x, t[nt][2].y),
+                          vmax(t[nt][3].x, t[nt][3].y));
+    const float rel = rows_max(v);  // chunk max relative to the running max
+    mx[nt] = rel + m_eff;
+    grow |= first || rel > RESCALE_LOG2;
   }
   return __builtin_amdgcn_ballot_w64(grow) != 0;
 }
 
 template <int HD, int NT, bool F8, typename ReloadV>
-__device__ __forceinline__ void full_pv(Chunk<HD, F8>& c, const f32x4 (&s)[NT][2], float scale_log2,
-                                        const float (&m)[NT], float (&l)[NT], f32x4 (&o)[NT][HD / 16],
-                                        ReloadV reload_v) {
+__device__ __forceinline__ void full_pv(Chunk<HD, F8>& c, const f32x2 (&t)[NT][4], float (&l)[NT],
+                                        f32x4 (&o)[NT][HD / 16], ReloadV reload_v) {
   bf16x8 bp[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
-    float ps = 0.f;
+    f32x2 p[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float pj = fast_exp2(s[nt][j >> 2][j & 3] * scale_log2 - m[nt]);
-      ps += pj;
-      bp[nt][j] = static_cast<__bf16>(pj);
+    for (int q = 0; q < 4; ++q) {
+      p[q] = f32x2{fast_exp2(t[nt][q].x), fast_exp2(t[nt][q].y)};
+      bp[nt][2 * q] = static_cast<__bf16>(p[q].x);
+      bp[nt][2 * q + 1] = static_cast<__bf16>(p[q].y);
     }
-    l[nt] += rows_sum(ps);
+    const f32x2 ps2 = (p[0] + p[1]) + (p[2] + p[3]);  // packed adds
+    l[nt] += rows_sum(ps2.x + ps2.y);
   }
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
@@ -305,16 +331,23 @@ __device__ __forceinline__ void full_pv(Chunk<HD, F8>& c, const f32x4 (&s)[NT][2
   reload_v(c);
 }
 
+// The (rare) lazy rescale: the running max moves to the chunk max; O and l scale by 2^(m - m_new)
+// and the chunk's relative scores t shift by the same amount.
 template <int HD, int NT>
 __device__ __forceinline__ void full_rescale(const float (&mx)[NT], float (&m)[NT], float (&l)[NT],
-                                             f32x4 (&o)[NT][HD / 16]) {
+                                             f32x4 (&o)[NT][HD / 16], f32x2 (&t)[NT][4]) {
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
-    const float m_new = fmaxf(m[nt], mx[nt]);
-    const float alpha = m[nt] == -INFINITY ? 0.f : fast_exp2(m[nt] - m_new);
+    const bool first = m[nt] == -INFINITY;
+    const float m_new = first ? mx[nt] : fmaxf(m[nt], mx[nt]);
+    const float alpha = first ? 0.f : fast_exp2(m[nt] - m_new);
     l[nt] *= alpha;
 #pragma unroll
     for (int dt = 0; dt < HD / 16; ++dt) o[nt][dt] *= alpha;
+    const float shift = m_new - (first ? 0.f : m[nt]);  // t was relative to m_eff (full_scores)
+    const f32x2 sh = {shift, shift};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[nt][q] -= sh;
     m[nt] = m_new;
   }
 }
@@ -612,22 +645,22 @@ __global__ __launch_bounds__(64 * SH_WAVES) void decode_shared_kernel(
     Chunk<HD, F8> cur;
     load_chunk<HD, F8>(cur, g, table[2 * c], table[min(2 * c + 1, nblk - 1)], kvh, lane);
     while (c < n_full) {
-      f32x4 s[NT][2];
+      f32x2 t[NT][4];
       float mx[NT];
       bool grow = false;
       int b0 = 0, b1 = 0;
       for (; c < n_full; ++c) {
         const int cn = min(c + 1, nchunk - 1);
         b0 = table[2 * cn], b1 = table[min(2 * cn + 1, nblk - 1)];
-        grow = full_scores<HD, NT, F8>(cur, bq, scale_log2, m, s, mx,
+        grow = full_scores<HD, NT, F8>(cur, bq, scale_log2, m, t, mx,
                                        [&](Chunk<HD, F8>& x) { load_chunk_k<HD, F8>(x, g, b0, b1, kvh, lane); });
         if (grow) break;  // wave-uniform
-        full_pv<HD, NT, F8>(cur, s, scale_log2, m, l, o,
+        full_pv<HD, NT, F8>(cur, t, l, o,
                             [&](Chunk<HD, F8>& x) { load_chunk_v<HD, F8>(x, g, b0, b1, kvh, lane); });
       }
       if (!grow) break;
-      full_rescale<HD, NT>(mx, m, l, o);
-      full_pv<HD, NT, F8>(cur, s, scale_log2, m, l, o,
+      full_rescale<HD, NT>(mx, m, l, o, t);
+      full_pv<HD, NT, F8>(cur, t, l, o,
                           [&](Chunk<HD, F8>& x) { load_chunk_v<HD, F8>(x, g, b0, b1, kvh, lane); });
       ++c;
     }
@@ -800,7 +833,7 @@ __global__ __launch_bounds__(256) PREFILL_ATTR void prefill_attn_kernel(
   int c = 0;
   const int n_full = min(sub_first[0] / CHUNK, nchunk);  // chunks every row of the wave sees in full
   while (c < n_full) {
-    f32x4 s[NT][2];
+    f32x2 t[NT][4];
     float mx[NT];
     bool grow = false;
     int b0 = 0, b1 = 0;
@@ -809,15 +842,15 @@ __global__ __launch_bounds__(256) PREFILL_ATTR void prefill_attn_kernel(
     for (; c < n_full; ++c) {
       const int cn = min(c + 1, nchunk - 1);
       b0 = block_at(2 * cn), b1 = block_at(min(2 * cn + 1, nblk - 1));
-      grow = full_scores<HD, NT, F8>(cur, bq, scale_log2, m, s, mx,
+      grow = full_scores<HD, NT, F8>(cur, bq, scale_log2, m, t, mx,
                                      [&](Chunk<HD, F8>& x) { load_chunk_k<HD, F8>(x, g, b0, b1, kvh, lane); });
       if (grow) break;  // wave-uniform
-      full_pv<HD, NT, F8>(cur, s, scale_log2, m, l, o,
+      full_pv<HD, NT, F8>(cur, t, l, o,
                           [&](Chunk<HD, F8>& x) { load_chunk_v<HD, F8>(x, g, b0, b1, kvh, lane); });
     }
     if (!grow) break;
-    full_rescale<HD, NT>(mx, m, l, o);
-    full_pv<HD, NT, F8>(cur, s, scale_log2, m, l, o,
+    full_rescale<HD, NT>(mx, m, l, o, t);
+    full_pv<HD, NT, F8>(cur, t, l, o,
                         [&](Chunk<HD, F8>& x) { load_chunk_v<HD, F8>(x, g, b0, b1, kvh, lane); });
     ++c;
   }

@@ -19,6 +19,6 @@ for T in (3000, 9000, 16384):
     print(f"{tag} silu_mul T={T}: {us:.1f} us, {T * 17408 * 6 / us / 1e6:.2f} TB/s", flush=True)
 PY
 for r in 1 2; do
-  BCG_KERNELS_LIB=$PWD/build/libbcg_silu_old.so timeout -k 10 120 python /tmp/silu_time.py || exit 1
+  BCG_KERNELS_LIB=$PWD/build/libbcg_silu_old.so PYTHONPATH=$PWD timeout -k 10 120 python /tmp/silu_time.py || exit 1
   timeout -k 10 120 python /tmp/silu_time.py || exit 1
 done
