@@ -20,5 +20,5 @@ for T in (3000, 9000, 16384):
 PY
 for r in 1 2; do
   BCG_KERNELS_LIB=$PWD/build/libbcg_silu_old.so PYTHONPATH=$PWD timeout -k 10 120 python /tmp/silu_time.py || exit 1
-  timeout -k 10 120 python /tmp/silu_time.py || exit 1
+  PYTHONPATH=$PWD timeout -k 10 120 python /tmp/silu_time.py || exit 1
 done
