@@ -73,35 +73,22 @@ __global__ __launch_bounds__(NORM_THREADS) void add_rmsnorm_kernel(
 
 // One 16-B vector of gate + up per thread and grid row-major over [T, I/8]: 32-bit
 // index math (a 64-bit div/mod per element was the kernel's main cost), fast exp.
-constexpr int SILU_ROWS = 4;
-
 __global__ __launch_bounds__(256) void silu_mul_kernel(const bf16_t* __restrict__ gu,
                                                        bf16_t* __restrict__ out, int T, int I) {
-  // SILU_ROWS rows per iteration with all their loads issued first: one 16-B gate/up pair in
-  // flight per thread left the kernel latency-bound at ~5 TB/s
   const int nvec_row = I >> 3;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;  // vector within the row
   if (c >= nvec_row) return;
-  for (int r0 = blockIdx.y * SILU_ROWS; r0 < T; r0 += gridDim.y * SILU_ROWS) {
-    u16x8 gv[SILU_ROWS], uv[SILU_ROWS];
+  for (int r = blockIdx.y; r < T; r += gridDim.y) {
+    const bf16_t* g = gu + static_cast<size_t>(r) * 2 * I + c * 8;
+    const u16x8 gv = *reinterpret_cast<const u16x8*>(g);
+    const u16x8 uv = *reinterpret_cast<const u16x8*>(g + I);
+    u16x8 o;
 #pragma unroll
-    for (int i = 0; i < SILU_ROWS; ++i) {
-      const int r = min(r0 + i, T - 1);  // clamped rows are loaded, never stored
-      const bf16_t* g = gu + static_cast<size_t>(r) * 2 * I + c * 8;
-      gv[i] = *reinterpret_cast<const u16x8*>(g);
-      uv[i] = *reinterpret_cast<const u16x8*>(g + I);
+    for (int j = 0; j < 8; ++j) {
+      const float a = bf2f(gv[j]);
+      o[j] = f2bf(__fdividef(a, 1.f + __expf(-a)) * bf2f(uv[j]));
     }
-#pragma unroll
-    for (int i = 0; i < SILU_ROWS; ++i) {
-      if (r0 + i >= T) break;
-      u16x8 o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float a = bf2f(gv[i][j]);
-        o[j] = f2bf(__fdividef(a, 1.f + __expf(-a)) * bf2f(uv[i][j]));
-      }
-      *reinterpret_cast<u16x8*>(out + static_cast<size_t>(r0 + i) * I + c * 8) = o;
-    }
+    *reinterpret_cast<u16x8*>(out + static_cast<size_t>(r) * I + c * 8) = o;
   }
 }
 
@@ -132,7 +119,7 @@ BCG_API int bcg_silu_mul(const void* gu, void* out, int64_t T, int I, hipStream_
   if (I % 8 != 0 || T <= 0) return -2;
   if (T > (1 << 30) || I > (1 << 27)) return -2;
   const int bx = (I / 8 + 255) / 256;
-  const int by = static_cast<int>(std::min<int64_t>((T + SILU_ROWS - 1) / SILU_ROWS, std::max<int64_t>(1, 8192 / bx)));
+  const int by = static_cast<int>(std::min<int64_t>(T, std::max<int64_t>(1, 8192 / bx)));
   hipLaunchKernelGGL(silu_mul_kernel, dim3(bx, by), dim3(256), 0, stream,
                      static_cast<const bf16_t*>(gu), static_cast<bf16_t*>(out), static_cast<int>(T), I);
   return BCG_CHECK_LAUNCH();
