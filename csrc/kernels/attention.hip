@@ -841,7 +841,11 @@ __global__ __launch_bounds__(256) PREFILL_ATTR void prefill_attn_kernel(
     // when a column's max moved enough to need the lazy rescale
     for (; c < n_full; ++c) {
       const int cn = min(c + 1, nchunk - 1);
+#ifdef PREFILL_ABL_HOT  // timing ablation only (wrong results): every reload re-reads chunk 0's blocks (L2-hot)
+      b0 = block_at(0), b1 = block_at(min(1, nblk - 1));
+#else
       b0 = block_at(2 * cn), b1 = block_at(min(2 * cn + 1, nblk - 1));
+#endif
       grow = full_scores<HD, NT, F8>(cur, bq, scale_log2, m, t, mx,
                                      [&](Chunk<HD, F8>& x) { load_chunk_k<HD, F8>(x, g, b0, b1, kvh, lane); });
       if (grow) break;  // wave-uniform
