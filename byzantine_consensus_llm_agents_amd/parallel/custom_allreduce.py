@@ -37,6 +37,31 @@ def choose_mode(nbytes: int, world: int, oneshot_max: int = ONESHOT_MAX) -> int:
     return 1 if nbytes <= limit else 2
 
 
+def pick_thresholds(sizes: List[int], t_one: List[float], t_two: List[float], t_rccl: List[float],
+                    cap_bytes: int):
+    """Routing limits from a measured table (bytes -> us per call, identical on every rank).
+
+    Returns ``(oneshot_limit, route_max)``: one-shot up to the largest measured size at which it
+    still beats two-shot (0: two-shot from the smallest size on), the custom kernels up to the
+    largest measured size at which the better of them beats RCCL (RCCL beyond; ``cap_bytes`` when
+    they win everywhere).  Both limits are measured sizes (no extrapolation), and only a prefix
+    of wins counts: above the first size where a method loses, the other one is used.
+    """
+    oneshot_limit = 0
+    for nb, a, b in zip(sizes, t_one, t_two):
+        if a > b:
+            break
+        oneshot_limit = nb
+    route_max = 0
+    for nb, a, b, r in zip(sizes, t_one, t_two, t_rccl):
+        if min(a, b) > r:
+            break
+        route_max = nb
+    if route_max == sizes[-1]:
+        route_max = cap_bytes
+    return oneshot_limit, route_max
+
+
 def choose_blocks(nbytes: int, world: int, mode: int, max_blocks: int = 128) -> int:
     """Workgroups per call: ~2 16-B vectors per thread per block, capped at `max_blocks`."""
     nvec = max(1, nbytes // 16)
@@ -86,19 +111,26 @@ class _Rank:
             raise ValueError(f"custom all-reduce supports power-of-two groups of <= {mr.value} ranks")
         self.max_blocks = mb.value
         self.calls = {1: 0, 2: 0}
+        self.route_max = cap_bytes   # messages routed to the kernels (RCCL above); calibrate() may lower it
+        self.oneshot_limit = None    # measured one-shot limit (None: the choose_mode rule)
+        self.calibration = None
 
     def can(self, x: torch.Tensor) -> bool:
         n = x.numel()
         return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and n > 0 and n % 8 == 0
-                and 2 * n <= self.cap_bytes)
+                and 2 * n <= min(self.cap_bytes, self.route_max))
 
-    def all_reduce_(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
-        """In-place (or into `out`) sum over the group, on the current (or given) HIP stream."""
+    def all_reduce_(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, stream=None,
+                    mode: Optional[int] = None) -> torch.Tensor:
+        """In-place (or into `out`) sum over the group, on the current (or given) HIP stream.
+        `mode` (1 = one-shot, 2 = two-shot) overrides the routing rule (calibration)."""
         if not self.can(x):
             raise ValueError("custom all-reduce: need contiguous bf16 on the GPU, numel % 8 == 0, <= cap")
         out = x if out is None else out
         nbytes = 2 * x.numel()
-        mode = choose_mode(nbytes, self.world, self.oneshot_max)
+        if mode is None:
+            mode = (choose_mode(nbytes, self.world, self.oneshot_max) if self.oneshot_limit is None
+                    else 1 if nbytes <= self.oneshot_limit else 2)
         blocks = choose_blocks(nbytes, self.world, mode, self.max_blocks)
         s = (stream or torch.cuda.current_stream()).cuda_stream
         rc = self.lib.bcg_ar_allreduce(self._data, self._sig, self.rank, self.world,
@@ -109,6 +141,42 @@ class _Rank:
             raise RuntimeError(f"bcg_ar_allreduce launch failed (rc={rc})")
         self.calls[mode] += 1
         return out
+
+    def calibrate(self, group, sizes: Optional[List[int]] = None, iters: int = 20, route: bool = True) -> dict:
+        """Measure one-shot, two-shot and RCCL (``dist.all_reduce`` on `group`) on this group's
+        own links at a few message sizes and set the routing limits from the table
+        (``pick_thresholds``).  Collective over the group; the timings are max-reduced first, so
+        every rank routes identically.  Replaces the built-in guesses (``ONESHOT_MAX``, halved at
+        8 ranks; the buffer cap) with what this node's xGMI topology measures.  ``route=False``
+        keeps the kernels' range (gloo groups chunk large messages through them)."""
+        import torch.distributed as dist
+        sizes = sizes or [nb for nb in (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20) if nb <= self.cap_bytes]
+        dev = torch.device("cuda", torch.cuda.current_device())
+        table = torch.zeros(3, len(sizes), dtype=torch.float64, device=dev)
+        for i, nb in enumerate(sizes):
+            x = torch.zeros(nb // 2, dtype=torch.bfloat16, device=dev)
+            fns = (lambda: self.all_reduce_(x, mode=1), lambda: self.all_reduce_(x, mode=2),
+                   lambda: dist.all_reduce(x, group=group))
+            for m, fn in enumerate(fns):
+                fn()
+                torch.cuda.synchronize()
+                dist.barrier(group=group)
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(iters):
+                    fn()
+                b.record()
+                b.synchronize()
+                table[m, i] = a.elapsed_time(b) * 1e3 / iters
+        dist.all_reduce(table, op=dist.ReduceOp.MAX, group=group)
+        t = table.cpu().tolist()
+        self.oneshot_limit, route_max = pick_thresholds(sizes, t[0], t[1], t[2], self.cap_bytes)
+        if route:
+            self.route_max = route_max
+        self.calls = {1: 0, 2: 0}
+        self.calibration = {"sizes": sizes, "oneshot_us": t[0], "twoshot_us": t[1], "rccl_us": t[2],
+                            "oneshot_limit": self.oneshot_limit, "route_max": route_max}
+        return self.calibration
 
     def error_async(self, host: torch.Tensor, stream) -> None:
         """Queue a copy of this rank's error word into pinned int32 `host[0]` on `stream`."""

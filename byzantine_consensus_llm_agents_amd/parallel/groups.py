@@ -122,6 +122,11 @@ def tensor_parallel_group(tp: int, custom_allreduce: bool = False) -> TPGroup:
             # larger messages go through the kernels in cap-sized pieces, TPGroup.chunk_large)
             _CUSTOM_AR[tp] = XGMIAllReduce(_TP_GROUPS[tp], cap_bytes=int(os.environ.get("BCG_AR_CAP_MB", "32")) << 20,
                                            timeout_s=float(os.environ.get("BCG_AR_TIMEOUT_S", "30")))
+            # routing limits measured on this group's links (RCCL groups; BCG_AR_CALIBRATE=0 keeps the
+            # built-in rule, =force also calibrates over gloo -- one-GPU tests of the mechanism)
+            cal = os.environ.get("BCG_AR_CALIBRATE", "1")
+            if cal == "force" or (cal != "0" and dist.get_backend(_TP_GROUPS[tp]) == "nccl"):
+                _CUSTOM_AR[tp].calibrate(_TP_GROUPS[tp], route=dist.get_backend(_TP_GROUPS[tp]) == "nccl")
         custom = _CUSTOM_AR[tp]
     return TPGroup(_TP_GROUPS[tp], lay.tp_rank, tp, custom=custom, ctrl=_TP_CTRL[tp],
                    leader=lay.rank - lay.tp_rank, chunk_large=dist.get_backend(_TP_GROUPS[tp]) == "gloo")

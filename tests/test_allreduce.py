@@ -33,6 +33,19 @@ def test_choose_mode_and_blocks():
             assert 1 <= b <= 128
 
 
+def test_pick_thresholds_from_measured_table():
+    sizes = [64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20]
+    one = [10, 20, 60, 300, 1300]
+    two = [14, 22, 50, 180, 700]
+    rccl = [40, 45, 70, 170, 500]
+    # one-shot wins up to 256 KiB; the kernels beat RCCL up to 1 MiB (two-shot 50 < 70), lose at 4 MiB
+    assert CA.pick_thresholds(sizes, one, two, rccl, 32 << 20) == (256 << 10, 1 << 20)
+    # kernels win everywhere: the buffer cap stays the limit; one-shot never wins: 0
+    assert CA.pick_thresholds(sizes, [9] * 5, [5] * 5, [99] * 5, 32 << 20) == (0, 32 << 20)
+    # only a prefix of wins counts (a win above the first loss is measurement noise)
+    assert CA.pick_thresholds(sizes, [1, 9, 1, 1, 1], [5] * 5, [99] * 5, 32 << 20)[0] == 64 << 10
+
+
 class _FakeCustom:
     def __init__(self, accept):
         self.accept, self.calls = accept, 0
@@ -121,12 +134,20 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _ipc_worker(rank, world, port, out):
+def _ipc_worker(rank, world, port, out, calibrate=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     import torch.distributed as dist
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     ar = CA.XGMIAllReduce(dist.group.WORLD, cap_bytes=4 << 20, timeout_s=5.0)
+    cal = None
+    if calibrate:  # the measured-routing path (timings on one GPU are not xGMI's: only the mechanics)
+        cal = ar.calibrate(dist.group.WORLD, sizes=[64 << 10, 1 << 20], iters=3, route=False)
+        cal = {"limit_ok": cal["oneshot_limit"] in (0, 64 << 10, 1 << 20), "same": None,
+               "limit": cal["oneshot_limit"]}
+        lims = [None] * world
+        dist.all_gather_object(lims, cal["limit"])
+        cal["same"] = len(set(lims)) == 1  # every rank routes identically (max-reduced table)
     ok = []
     for n in (4096, 5120 * 40, 5120 * 150):  # one-shot, one-shot, two-shot (1.5 MiB)
         gen = torch.Generator().manual_seed(1000 + n)  # every rank can rebuild every input
@@ -141,20 +162,23 @@ def _ipc_worker(rank, world, port, out):
     dist.barrier()
     ar.close()
     with open(f"{out}.{rank}", "w") as fh:
-        json.dump({"ok": ok, "err": err}, fh)
+        json.dump({"ok": ok, "err": err, **({"cal": cal} if calibrate else {})}, fh)
     dist.destroy_process_group()
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4])
-def test_ipc_processes_one_gpu(tmp_path, world):
-    """`world` processes (own HIP queues each) on one GPU, buffers mapped through hipIpc."""
+@pytest.mark.parametrize("world,calibrate", [(2, False), (4, False), (2, True)])
+def test_ipc_processes_one_gpu(tmp_path, world, calibrate):
+    """`world` processes (own HIP queues each) on one GPU, buffers mapped through hipIpc;
+    calibrate: routing limits measured first (XGMIAllReduce.calibrate), then the same checks."""
     out = str(tmp_path / "ar")
-    mp.start_processes(_ipc_worker, args=(world, _free_port(), out), nprocs=world, join=True,
+    mp.start_processes(_ipc_worker, args=(world, _free_port(), out, calibrate), nprocs=world, join=True,
                        start_method="spawn")
     for r in range(world):
         res = json.load(open(f"{out}.{r}"))
-        assert res == {"ok": [True, True, True], "err": False}, (r, res)
+        assert res["ok"] == [True, True, True] and res["err"] is False, (r, res)
+        if calibrate:
+            assert res["cal"]["limit_ok"] and res["cal"]["same"], (r, res)
 
 
 def _tp_worker(rank, world, port, out, back_to_back, cap_mb):
