@@ -752,7 +752,7 @@ void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
 #define PREFILL_WPE 0
 #endif
 #if PREFILL_WPE
-#define PREFILL_ATTR __attribute__((amdgpu_waves_per_eu(1, 1)))
+#define PREFILL_ATTR __attribute__((amdgpu_waves_per_eu(PREFILL_WPE, PREFILL_WPE)))
 #else
 #define PREFILL_ATTR
 #endif
@@ -899,7 +899,10 @@ template <int HD, bool F8>
 void launch_prefill(int n_tiles, int n_q, const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
                     const int* q_start, const int* seq_lens, const int* tiles, float sl, bf16_t* out,
                     hipStream_t stream) {
-  constexpr int NT = 4;  // 1 and 2 measured slower (PERF.md); the LDS-shared forms were 180-200 TF/s
+#ifndef PREFILL_NT
+#define PREFILL_NT 4
+#endif
+  constexpr int NT = PREFILL_NT;  // 1 and 2 measured slower (PERF.md); the LDS-shared forms were 180-200 TF/s
   const int hg_n = (n_q + NT - 1) / NT;
   static const int xcd_order = [] {
     const char* e = std::getenv("BCG_PREFILL_XCD_ORDER");
