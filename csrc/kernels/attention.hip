@@ -745,6 +745,9 @@ void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
 #ifndef PREFILL_FULL_BLOCK
 #define PREFILL_FULL_BLOCK 1  // fully visible chunks through full_scores / full_pv (lazy rescale outside the inner loop, in-place reload)
 #endif
+#ifndef PREFILL_LDS
+#define PREFILL_LDS 0  // shared K/V ring (LDSKV); BCG_PREFILL_LDS=0/1 overrides at run time
+#endif
 #ifndef PREFILL_XCD_ORDER
 #define PREFILL_XCD_ORDER 0  // default grid order (BCG_PREFILL_XCD_ORDER=0/1 overrides at run time)
 #endif
@@ -756,7 +759,15 @@ void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
 #else
 #define PREFILL_ATTR
 #endif
-template <int HD, int NT, bool F8 = false>
+// LDSKV (bf16 cache, HD = 128, NT = 4): the 4 waves of a workgroup are 4 consecutive query heads
+// (at most 2 kv heads when G >= 2); each 32-token chunk of both kv heads' K and V goes global -> LDS
+// ONCE per workgroup by LDS-DMA (8 x 1-KiB pieces per wave), 4-slot ring, issued 2 chunks ahead;
+// the in-place reloads of the full-visibility loop then read their fragments from LDS
+// (XOR-swizzled K rows: conflict-free ds_read_b128) instead of issuing 16 global loads per wave.
+// One raw s_barrier per chunk (all waves share the rows, so they run the same chunks).
+__device__ __forceinline__ int kswz(int row) { return ((row & 3) | ((row & 8) >> 1)) << 1; }
+
+template <int HD, int NT, bool F8 = false, bool LDSKV = false>
 __global__ __launch_bounds__(256) PREFILL_ATTR void prefill_attn_kernel(
     const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
     const int* __restrict__ q_start, const int* __restrict__ seq_lens, const int* __restrict__ tiles,
@@ -832,31 +843,124 @@ __global__ __launch_bounds__(256) PREFILL_ATTR void prefill_attn_kernel(
   // second register set for the prefetch
   int c = 0;
   const int n_full = min(sub_first[0] / CHUNK, nchunk);  // chunks every row of the wave sees in full
-  while (c < n_full) {
-    f32x2 t[NT][4];
-    float mx[NT];
-    bool grow = false;
-    int b0 = 0, b1 = 0;
-    // inner loop: no VALU on O (it stays in the MFMA accumulators); leaves with S live
-    // when a column's max moved enough to need the lazy rescale
-    for (; c < n_full; ++c) {
-      const int cn = min(c + 1, nchunk - 1);
+
+  // ---- LDSKV: shared K/V ring (see above the kernel) ----
+  constexpr int KV_SLOTS = 4, KV_HALF = 8192, KV_HEAD = 2 * KV_HALF, KV_SLOT = 2 * KV_HEAD;
+  __shared__ __attribute__((aligned(1024))) unsigned char kv_ring[LDSKV ? KV_SLOTS * KV_SLOT : 16];
+  const int kvA = LDSKV ? (hgrp * NT) / (n_q / g.n_kv) : 0;
+  const int kvsel = kvh - kvA;                                              // which staged kv head this wave reads
+  const int dkv = min(kvA + (w >> 1), (hgrp * NT + NT - 1) / (n_q / g.n_kv));  // kv head this wave stages
+  // block ids of the DMA lookahead: scalar loads (lgkmcnt) -- a vector load here would make every
+  // wait on it (vmcnt counts in order) drain the DMA pieces in flight ahead of it
+  auto block_at2 = [&](int bi) -> int { return table[__builtin_amdgcn_readfirstlane(bi)]; };
+  auto issue_chunk = [&](int k) {  // this wave's 8 pieces (K or V of kv head dkv) of chunk k
+    if constexpr (LDSKV && !F8) {
+      const int bb0 = block_at2(2 * k), bb1 = block_at2(min(2 * k + 1, nblk - 1));
+      unsigned char* dst = kv_ring + (k % KV_SLOTS) * KV_SLOT + (w >> 1) * KV_HEAD + (w & 1) * KV_HALF;
+      const unsigned char* kc = reinterpret_cast<const unsigned char*>(g.k);
+      const unsigned char* vc = reinterpret_cast<const unsigned char*>(g.v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const size_t base = 2 * block_base<HD>(g, i < 4 ? bb0 : bb1, dkv);
+        const unsigned char* src;
+        if ((w & 1) == 0) {  // K rows (i & 3) * 4 + lane / 16; the lane's LDS slot p holds chunk p ^ kswz(row)
+          const int row = (i & 3) * 4 + (lane >> 4);
+          src = kc + base + row * 256 + ((lane & 15) ^ kswz(row)) * 16;
+        } else {  // V^T: a plain copy of the block-head's 4 KiB
+          src = vc + base + (i & 3) * 1024 + lane * 16;
+        }
+        __builtin_amdgcn_global_load_lds(src, dst + i * 1024, 16, 0, 0);
+      }
+    }
+  };
+  auto lds_k = [&](Chunk<HD, F8>& x, int k) {
+    if constexpr (LDSKV && !F8) {
+      const unsigned char* base = kv_ring + (k % KV_SLOTS) * KV_SLOT + kvsel * KV_HEAD;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int t = 8 * (r >> 2) + 4 * u + (r & 3), row = t & 15;
+#pragma unroll
+        for (int kk = 0; kk < HD / 32; ++kk)
+          x.k[u][kk] =
+              *reinterpret_cast<const bf16x8*>(base + (t >> 4) * 4096 + row * 256 + ((4 * kk + h) ^ kswz(row)) * 16);
+      }
+    }
+  };
+  auto lds_v = [&](Chunk<HD, F8>& x, int k) {
+    if constexpr (LDSKV && !F8) {
+      const unsigned char* base =
+          kv_ring + (k % KV_SLOTS) * KV_SLOT + kvsel * KV_HEAD + KV_HALF + (h >> 1) * 4096 + (h & 1) * 16;
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) x.v[dt] = *reinterpret_cast<const bf16x8*>(base + (dt * 16 + r) * 32);
+    }
+  };
+  if constexpr (LDSKV && !F8) {  // chunks 1 and 2 ahead of the loop; chunk k + 3 is issued in iteration k
+    if (1 < min(n_full + 1, nchunk)) issue_chunk(1);
+    if (2 < min(n_full + 1, nchunk)) issue_chunk(2);
+  }
+  // LDSKV: chunks 1 .. n_stage-1 go through the ring -- every full chunk's successor, including
+  // the first masked chunk, which the masked loop below then starts from
+  const int n_stage = min(n_full + 1, nchunk);
+  auto ring_k = [&](Chunk<HD, F8>& x) {
+    if (c + 1 >= n_stage) return;  // no successor (the wave's last chunk): nothing to reload
+    // this wave's pieces of chunk c+1 landed (chunk c+2's 8 may still fly), then every wave's
+    if (c + 2 < n_stage) {
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // ... and every wave is past chunk c-1: its slot is free
+    asm volatile("" ::: "memory");
+    if (c + 3 < n_stage) issue_chunk(c + 3);
+    lds_k(x, c + 1);
+  };
+  auto ring_v = [&](Chunk<HD, F8>& x) {
+    if (c + 1 < n_stage) lds_v(x, c + 1);
+  };
+  if constexpr (LDSKV && !F8) {
+    // no VGPR-destination global load in this loop: with one, the compiler's wait before the
+    // S^T MFMAs would be a vmcnt(0) that drains the ring every chunk
+    while (c < n_full) {
+      f32x2 t[NT][4];
+      float mx[NT];
+      bool grow = false;
+      for (; c < n_full; ++c) {
+        grow = full_scores<HD, NT, F8>(cur, bq, scale_log2, m, t, mx, ring_k);
+        if (grow) break;  // wave-uniform
+        full_pv<HD, NT, F8>(cur, t, l, o, ring_v);
+      }
+      if (!grow) break;
+      full_rescale<HD, NT>(mx, m, l, o, t);
+      full_pv<HD, NT, F8>(cur, t, l, o, ring_v);
+      ++c;
+    }
+  } else {
+    while (c < n_full) {
+      f32x2 t[NT][4];
+      float mx[NT];
+      bool grow = false;
+      int b0 = 0, b1 = 0;
+      // inner loop: no VALU on O (it stays in the MFMA accumulators); leaves with S live
+      // when a column's max moved enough to need the lazy rescale
+      for (; c < n_full; ++c) {
+        const int cn = min(c + 1, nchunk - 1);
 #ifdef PREFILL_ABL_HOT  // timing ablation only (wrong results): every reload re-reads chunk 0's blocks (L2-hot)
-      b0 = block_at(0), b1 = block_at(min(1, nblk - 1));
+        b0 = block_at(0), b1 = block_at(min(1, nblk - 1));
 #else
-      b0 = block_at(2 * cn), b1 = block_at(min(2 * cn + 1, nblk - 1));
+        b0 = block_at(2 * cn), b1 = block_at(min(2 * cn + 1, nblk - 1));
 #endif
-      grow = full_scores<HD, NT, F8>(cur, bq, scale_log2, m, t, mx,
-                                     [&](Chunk<HD, F8>& x) { load_chunk_k<HD, F8>(x, g, b0, b1, kvh, lane); });
-      if (grow) break;  // wave-uniform
+        grow = full_scores<HD, NT, F8>(cur, bq, scale_log2, m, t, mx,
+                                       [&](Chunk<HD, F8>& x) { load_chunk_k<HD, F8>(x, g, b0, b1, kvh, lane); });
+        if (grow) break;  // wave-uniform
+        full_pv<HD, NT, F8>(cur, t, l, o,
+                            [&](Chunk<HD, F8>& x) { load_chunk_v<HD, F8>(x, g, b0, b1, kvh, lane); });
+      }
+      if (!grow) break;
+      full_rescale<HD, NT>(mx, m, l, o, t);
       full_pv<HD, NT, F8>(cur, t, l, o,
                           [&](Chunk<HD, F8>& x) { load_chunk_v<HD, F8>(x, g, b0, b1, kvh, lane); });
+      ++c;
     }
-    if (!grow) break;
-    full_rescale<HD, NT>(mx, m, l, o, t);
-    full_pv<HD, NT, F8>(cur, t, l, o,
-                        [&](Chunk<HD, F8>& x) { load_chunk_v<HD, F8>(x, g, b0, b1, kvh, lane); });
-    ++c;
   }
   Chunk<HD, F8> nxt;
   for (; c < nchunk; ++c) {
@@ -908,13 +1012,19 @@ void launch_prefill(int n_tiles, int n_q, const bf16_t* q, KVGeom g, const int* 
     const char* e = std::getenv("BCG_PREFILL_XCD_ORDER");
     return e ? std::atoi(e) : PREFILL_XCD_ORDER;
   }();
-  if (xcd_order) {
-    const int rounds = (n_tiles + 7) / 8;
-    hipLaunchKernelGGL((prefill_attn_kernel<HD, NT, F8>), dim3(rounds * 8 * hg_n), dim3(256), 0, stream, q, g,
-                       tables, max_blocks, q_start, seq_lens, tiles, n_q, sl, out, n_tiles, 1);
+  static const int lds_env = [] {
+    const char* e = std::getenv("BCG_PREFILL_LDS");
+    return e ? std::atoi(e) : PREFILL_LDS;
+  }();
+  // the shared K/V ring needs whole 4-head workgroups spanning <= 2 kv heads, HD = 128, bf16 KV
+  const bool lds = lds_env && HD == 128 && !F8 && NT == 4 && n_q % 4 == 0 && n_q / g.n_kv >= 2;
+  const dim3 grid = xcd_order ? dim3(((n_tiles + 7) / 8) * 8 * hg_n) : dim3(n_tiles, hg_n);
+  if (lds) {
+    hipLaunchKernelGGL((prefill_attn_kernel<HD, NT, F8, true>), grid, dim3(256), 0, stream, q, g, tables, max_blocks,
+                       q_start, seq_lens, tiles, n_q, sl, out, n_tiles, xcd_order);
   } else {
-    hipLaunchKernelGGL((prefill_attn_kernel<HD, NT, F8>), dim3(n_tiles, hg_n), dim3(256), 0, stream, q, g, tables,
-                       max_blocks, q_start, seq_lens, tiles, n_q, sl, out, n_tiles, 0);
+    hipLaunchKernelGGL((prefill_attn_kernel<HD, NT, F8, false>), grid, dim3(256), 0, stream, q, g, tables,
+                       max_blocks, q_start, seq_lens, tiles, n_q, sl, out, n_tiles, xcd_order);
   }
 }
 
