@@ -84,6 +84,8 @@ def build_kernels(force: bool = False, verbose: bool = False) -> str:
            f"-I{os.path.join(CSRC, 'kernels')}", *srcs, "-o", tmp]
     if os.environ.get("BCG_RESOURCE_USAGE"):
         cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
+    if os.environ.get("BCG_EXTRA_HIPFLAGS"):  # variant builds (tools), e.g. -DPREFILL_LDS_BUILD=1
+        cmd[1:1] = os.environ["BCG_EXTRA_HIPFLAGS"].split()
     out = _run(cmd)
     if verbose and out:
         print(out)

@@ -745,8 +745,11 @@ void launch_decode(const bf16_t* q, KVGeom g, const int* tables, int max_blocks,
 #ifndef PREFILL_FULL_BLOCK
 #define PREFILL_FULL_BLOCK 1  // fully visible chunks through full_scores / full_pv (lazy rescale outside the inner loop, in-place reload)
 #endif
+#ifndef PREFILL_LDS_BUILD
+#define PREFILL_LDS_BUILD 0  // compile the shared K/V ring form (LDSKV) into this library
+#endif
 #ifndef PREFILL_LDS
-#define PREFILL_LDS 0  // shared K/V ring (LDSKV); BCG_PREFILL_LDS=0/1 overrides at run time
+#define PREFILL_LDS 0  // with PREFILL_LDS_BUILD: use the ring by default; BCG_PREFILL_LDS=0/1 overrides at run time
 #endif
 #ifndef PREFILL_XCD_ORDER
 #define PREFILL_XCD_ORDER 0  // default grid order (BCG_PREFILL_XCD_ORDER=0/1 overrides at run time)
@@ -1019,13 +1022,17 @@ void launch_prefill(int n_tiles, int n_q, const bf16_t* q, KVGeom g, const int* 
   // the shared K/V ring needs whole 4-head workgroups spanning <= 2 kv heads, HD = 128, bf16 KV
   const bool lds = lds_env && HD == 128 && !F8 && NT == 4 && n_q % 4 == 0 && n_q / g.n_kv >= 2;
   const dim3 grid = xcd_order ? dim3(((n_tiles + 7) / 8) * 8 * hg_n) : dim3(n_tiles, hg_n);
+#if PREFILL_LDS_BUILD  // the shared-ring form lost its A/B: only variant builds carry it (-DPREFILL_LDS_BUILD=1)
   if (lds) {
     hipLaunchKernelGGL((prefill_attn_kernel<HD, NT, F8, true>), grid, dim3(256), 0, stream, q, g, tables, max_blocks,
                        q_start, seq_lens, tiles, n_q, sl, out, n_tiles, xcd_order);
-  } else {
-    hipLaunchKernelGGL((prefill_attn_kernel<HD, NT, F8, false>), grid, dim3(256), 0, stream, q, g, tables,
-                       max_blocks, q_start, seq_lens, tiles, n_q, sl, out, n_tiles, xcd_order);
+    return;
   }
+#else
+  (void)lds;
+#endif
+  hipLaunchKernelGGL((prefill_attn_kernel<HD, NT, F8, false>), grid, dim3(256), 0, stream, q, g, tables, max_blocks,
+                     q_start, seq_lens, tiles, n_q, sl, out, n_tiles, xcd_order);
 }
 
 }  // namespace

@@ -1,5 +1,7 @@
 #!/bin/bash
 # Prefill attention with the shared K/V ring (BCG_PREFILL_LDS=1): GPU tests, then A/B against the register form.
+# The ring form is not in the production library: build it first, e.g.
+#   BCG_EXTRA_HIPFLAGS=-DPREFILL_LDS_BUILD=1 python -m byzantine_consensus_llm_agents_amd.utils.build --force
 set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
