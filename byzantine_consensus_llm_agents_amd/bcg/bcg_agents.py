@@ -252,6 +252,9 @@ class BCGAgent(EngineAgent):
             self.vote_schema(), LLM_CONFIG["temperature_vote"], LLM_CONFIG["max_tokens_vote"], accept,
             lambda base, nxt: P.RETRY_VOTE.format(base=base, next=nxt, total=MAX_JSON_RETRIES,
                                                   options=P.quoted_options(options)))
+        # whether the vote came from a valid response (False: all attempts failed and the
+        # reference's default CONTINUE is returned) -- read by the decisions/s counter only
+        self.last_vote_valid = result is not None
         if result is None:
             verbose_print(f"❌ [{self.agent_id}] FAILED ALL {MAX_JSON_RETRIES} JSON ATTEMPTS - DEFAULTING TO CONTINUE")
             return False

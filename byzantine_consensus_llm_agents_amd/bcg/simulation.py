@@ -330,7 +330,8 @@ class BCGSimulation:
             votes = run_concurrently(self._engine_agent(), [
                 (lambda a=self.agents[aid]: a.vote_to_terminate(game_state)) for aid, _ in pending])
             for (aid, _), vote in zip(pending, votes):
-                results[aid] = {"_sequential_success": True, "vote": vote}
+                results[aid] = {"_sequential_success": True, "vote": vote,
+                                "_valid": getattr(self.agents[aid], "last_vote_valid", True)}
             return []
 
         results = self._ladder(jobs, LLM_CONFIG["temperature_vote"], LLM_CONFIG["max_tokens_vote"],
@@ -346,7 +347,10 @@ class BCGSimulation:
                 vote = False
                 self.log(f"  {aid}: votes CONTINUE (default - all attempts failed)")
             else:
-                self.counters["votes_accepted"] += 1
+                # a sequential vote that exhausted its attempts is the game's default CONTINUE:
+                # the game sees it exactly as the reference does, the counter does not
+                if res.get("_valid", True):
+                    self.counters["votes_accepted"] += 1
                 if res.get("_sequential_success"):
                     vote = res.get("vote", False)
                 else:

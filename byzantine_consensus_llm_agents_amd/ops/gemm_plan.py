@@ -30,9 +30,10 @@ from typing import Dict, Optional, Tuple
 TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "engine", "tuned",
                      "hand_gemm.json")
 TILES = ((128, 128), (64, 128), (128, 64), (256, 128), (64, 256), (64, 64), (32, 128),  # csrc/kernels/gemm.hip CFGS
-         (256, 128), (128, 256), (128, 128), (256, 256))
+         (256, 128), (128, 256), (128, 128), (256, 256), (256, 256))
 PP_CFG = 10  # csrc/kernels/gemm_pp.hip: 256 x 256 ping-pong tile, N only a multiple of 16
-BIG_CFGS = (PP_CFG,)  # 256 x 256 tiles (the register-staged form lost its A/B: csrc/experimental/gemm_rs.hip)
+W4_CFG = 11  # csrc/kernels/gemm_w4.hip: 256 x 256, four 128 x 128 waves (one per SIMD), LDS-DMA fed
+BIG_CFGS = (PP_CFG, W4_CFG)  # 256 x 256 tiles (the register-staged form lost its A/B: csrc/experimental/gemm_rs.hip)
 N_CFGS = len(TILES)
 SPLITS = (1, 2, 3, 4, 6, 8)
 
@@ -65,8 +66,9 @@ class GemmPlan:
         if cfg not in self.tiles or M <= 0 or K % 64 or K <= 0 or split_k < 1 or K // 64 < split_k:
             return False
         bn = self.tiles[cfg][1]
-        if cfg in BIG_CFGS:  # 32-bit buffer offsets: operands below 4 GiB
-            return (N % 16 == 0 and 2 * (M + 256) * K < 1 << 32 and 2 * (N + 256) * K < 1 << 32
+        if cfg in BIG_CFGS:  # 32-bit buffer offsets: operands below 4 GiB (W4: 2 GiB)
+            lim = 1 << (31 if cfg == W4_CFG else 32)
+            return (N % 16 == 0 and 2 * (M + 256) * K < lim and 2 * (N + 256) * K < lim
                     and (epi != 1 or (N % 2 == 0 and (N // 2) % 128 == 0)))
         if N % bn:
             return False

@@ -8,11 +8,17 @@
   seconds.  Both outputs sit inside the package so they travel to the GPU box
   with the repo snapshot.
 
-Builds are skipped when the output is newer than every source; concurrent
-builders (DP ranks) write to a temp file and ``os.replace`` it into place.
+Builds are skipped when the output is newer than every source and was built
+with the same flags (a ``.flags`` sidecar beside it); concurrent builders (DP
+ranks) write to a temp file and ``os.replace`` it into place.
+
+``BCG_EXTRA_HIPFLAGS`` (variant builds for A/B tools, e.g. ``-DPREFILL_LDS_BUILD=1``)
+never touches the production library: the variant goes to
+``build/libbcg_<hash of the flags>.so`` and is selected with ``BCG_KERNELS_LIB``.
 """
 
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -34,11 +40,27 @@ def kernels_target() -> str:
     return os.path.join(PKG, "ops", "libbcg_kernels.so")
 
 
-def _stale(target: str, sources) -> bool:
+def variant_target(flags: str) -> str:
+    """Where a build with extra hipcc flags goes (never the production library)."""
+    tag = hashlib.sha1(" ".join(flags.split()).encode()).hexdigest()[:12]
+    return os.path.join(REPO, "build", f"libbcg_{tag}.so")
+
+
+def _stale(target: str, sources, flags: str = "") -> bool:
     if not os.path.exists(target):
+        return True
+    stamp = target + ".flags"
+    recorded = open(stamp).read() if os.path.exists(stamp) else ""
+    if recorded != flags:  # built with other flags: rebuild
         return True
     t = os.path.getmtime(target)
     return any(os.path.getmtime(s) > t for s in sources)
+
+
+def _write_stamp(target: str, flags: str):
+    if flags or os.path.exists(target + ".flags"):
+        with open(target + ".flags", "w") as fh:
+            fh.write(flags)
 
 
 def _run(cmd):
@@ -71,10 +93,12 @@ def build_runtime(force: bool = False, verbose: bool = False) -> str:
 def build_kernels(force: bool = False, verbose: bool = False) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
-    target = kernels_target()
+    extra = " ".join(os.environ.get("BCG_EXTRA_HIPFLAGS", "").split())
+    target = variant_target(extra) if extra else kernels_target()
+    os.makedirs(os.path.dirname(target), exist_ok=True)
     if not srcs:
         raise RuntimeError("no HIP kernel sources found")
-    if not force and not _stale(target, srcs + hdrs):
+    if not force and not _stale(target, srcs + hdrs, extra):
         return target
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     fd, tmp = tempfile.mkstemp(suffix=".so", dir=os.path.dirname(target))
@@ -84,13 +108,14 @@ def build_kernels(force: bool = False, verbose: bool = False) -> str:
            f"-I{os.path.join(CSRC, 'kernels')}", *srcs, "-o", tmp]
     if os.environ.get("BCG_RESOURCE_USAGE"):
         cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
-    if os.environ.get("BCG_EXTRA_HIPFLAGS"):  # variant builds (tools), e.g. -DPREFILL_LDS_BUILD=1
-        cmd[1:1] = os.environ["BCG_EXTRA_HIPFLAGS"].split()
+    if extra:  # variant builds (tools), e.g. -DPREFILL_LDS_BUILD=1: a separate target
+        cmd[1:1] = extra.split()
     out = _run(cmd)
     if verbose and out:
         print(out)
     os.chmod(tmp, 0o755)
     os.replace(tmp, target)
+    _write_stamp(target, extra)
     return target
 
 

@@ -8,10 +8,14 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <vector>
 
 #ifndef GEMM_FN
 #define GEMM_FN bcg_gemm_pp  // or bcg_gemm_rs (csrc/kernels/gemm_rs.hip): same contract
+#endif
+#ifdef W4_STAMPS
+extern "C" int bcg_gemm_w4_stamps(void* host, int n);
 #endif
 extern "C" int GEMM_FN(int epi, const void* x, const void* w, const void* bias, const void* residual, void* c,
                        void* ws, void* counters, int M, int N, int K, int inter, int split_k, hipStream_t stream);
@@ -87,8 +91,31 @@ int main(int argc, char** argv) {
   float ms = 0;
   CK(hipEventElapsedTime(&ms, a, b));
   const double us = ms * 1e3 / iters;
+  char extra[256] = "";
+#ifdef W4_STAMPS
+  {  // per-wave cycles per K-tile of the last launch: medians over the stamped waves
+    std::vector<uint64_t> st(1 << 16);
+    CK(hipDeviceSynchronize());
+    if (bcg_gemm_w4_stamps(st.data(), 1 << 16) == 0) {
+      const int nw = std::min(tiles * split, 4096) * 4;
+      std::vector<double> a, wt, b;
+      for (int i = 0; i < nw; ++i) {
+        const uint64_t* e = &st[i * 4];
+        if (!e[3]) continue;
+        a.push_back((double)e[0] / e[3]), wt.push_back((double)e[1] / e[3]), b.push_back((double)e[2] / e[3]);
+      }
+      auto med = [](std::vector<double>& v) {
+        if (v.empty()) return 0.0;
+        std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+        return v[v.size() / 2];
+      };
+      snprintf(extra, sizeof extra, ", \"cyc_per_ktile\": {\"phaseA\": %.0f, \"wait_barrier\": %.0f, \"phaseB\": %.0f}",
+               med(a), med(wt), med(b));
+    }
+  }
+#endif
   printf("{\"variant\": \"%s\", \"M\": %d, \"N\": %d, \"K\": %d, \"epi\": %d, \"split\": %d, \"us\": %.1f, "
-         "\"tflops\": %.1f}\n",
-         VARIANT_NAME, M, N, K, epi, split, us, 2.0 * M * N * K / us / 1e6);
+         "\"tflops\": %.1f%s}\n",
+         VARIANT_NAME, M, N, K, epi, split, us, 2.0 * M * N * K / us / 1e6, extra);
   return 0;
 }

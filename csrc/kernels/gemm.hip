@@ -385,10 +385,13 @@ int dispatch(int cfg, const void* x, const void* w, const void* bias, const void
 BCG_API int bcg_gemm_pp(int epi, const void* x, const void* w, const void* bias, const void* residual, void* c,
                         void* ws, void* counters, int M, int N, int K, int inter, int split_k, hipStream_t stream);
 constexpr int PP_CFG = N_CFG;  // the 256 x 256 ping-pong kernel (gemm_pp.hip)
+BCG_API int bcg_gemm_w4(int epi, const void* x, const void* w, const void* bias, const void* residual, void* c,
+                        void* ws, void* counters, int M, int N, int K, int inter, int split_k, hipStream_t stream);
+constexpr int W4_CFG = N_CFG + 1;  // 256 x 256, four 128 x 128 waves, LDS-DMA fed (gemm_w4.hip)
 
 // Tile configurations: see CFGS (BM x BN, pipeline stages); PP_CFG = gemm_pp.hip.
 BCG_API int bcg_gemm_tile(int cfg, int* bm, int* bn) {
-  if (cfg == PP_CFG) {
+  if (cfg == PP_CFG || cfg == W4_CFG) {
     *bm = *bn = 256;
     return 0;
   }
@@ -398,7 +401,7 @@ BCG_API int bcg_gemm_tile(int cfg, int* bm, int* bn) {
   return 0;
 }
 
-BCG_API int bcg_gemm_num_cfgs() { return N_CFG + 1; }
+BCG_API int bcg_gemm_num_cfgs() { return N_CFG + 2; }
 
 // epi: 0 = store (+bias), 1 = silu(gate)*up into [M, inter], 2 = residual + acc.
 // split_k > 1: fp32 partial tiles in `ws` (>= m_tiles*n_tiles*split_k*BM*BN floats) and one
@@ -409,6 +412,7 @@ BCG_API int bcg_gemm_nt(int cfg, int epi, const void* x, const void* w, const vo
                         void* c, void* ws, void* counters, int M, int N, int K, int inter, int split_k,
                         hipStream_t stream) {
   if (cfg == PP_CFG) return bcg_gemm_pp(epi, x, w, bias, residual, c, ws, counters, M, N, K, inter, split_k, stream);
+  if (cfg == W4_CFG) return bcg_gemm_w4(epi, x, w, bias, residual, c, ws, counters, M, N, K, inter, split_k, stream);
   if (M <= 0 || K % BK || K <= 0 || split_k < 1 || K / BK < split_k) return -2;
   if (split_k > 1 && (!ws || !counters)) return -2;
   int bm, bn;

@@ -57,7 +57,7 @@ def test_gemm_silu_mul_epilogue(hip, cfg, M, I, K):
     _close(h, ref)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 3, 10])
+@pytest.mark.parametrize("cfg", [0, 1, 3, 10, 11])
 def test_gemm_residual_epilogue_in_place(hip, cfg):
     torch.manual_seed(cfg)
     M, N, K = 77, 512, 2048
@@ -71,7 +71,7 @@ def test_gemm_residual_epilogue_in_place(hip, cfg):
 
 
 @pytest.mark.parametrize("cfg,split", [(0, 2), (5, 3), (6, 4), (2, 8), (1, 6), (7, 2), (9, 3), (10, 2), (10, 3),
-                                       (10, 5)])
+                                       (10, 5), (11, 2), (11, 3), (11, 5)])
 @pytest.mark.parametrize("epi", [0, 1, 2])
 def test_gemm_split_k(hip, cfg, split, epi):
     """Split-K with the in-kernel last-arriver reduction, repeated launches (the counters
@@ -111,9 +111,9 @@ def test_fused_ops_match_unfused(hip):
 @pytest.mark.parametrize("M,N,K", [(300, 1040, 64), (257, 528, 128), (513, 784, 192), (1, 4112, 320),
                                    (768, 2048, 1024)])
 @pytest.mark.parametrize("epi", [0, 2])
-@pytest.mark.parametrize("cfg", [10])
+@pytest.mark.parametrize("cfg", [10, 11])
 def test_gemm_pp_edges(hip, M, N, K, epi, cfg):
-    """The 256x256 ping-pong kernel (cfg 10) at its edges: 1-3
+    """The 256x256 kernels (cfg 10 ping-pong, cfg 11 four-wave) at their edges: 1-3
     K-tiles (prologue-only pipelines), M and N not multiples of the tile (clamped / range-checked
     loads, masked stores: the LM head has N = 151936 = 593.5 tiles), repeated launches."""
     torch.manual_seed(M * 7 + N + K)
@@ -131,7 +131,7 @@ def test_gemm_pp_edges(hip, M, N, K, epi, cfg):
         _close(got, want)
 
 
-@pytest.mark.parametrize("cfg", [10])
+@pytest.mark.parametrize("cfg", [10, 11])
 def test_gemm_pp_prefill_chunk_silu(hip, cfg):
     """A prefill-sized gate_up chunk through the 256x256 kernels with the fused SiLU*mul."""
     torch.manual_seed(5)

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--m", default="448,768,16384")
     ap.add_argument("--splits", default="1,2,3,4")
+    ap.add_argument("--cfgs", default="10,11", help="256x256 kernels to time: 10 ping-pong, 11 four-wave")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default="")
     args = ap.parse_args()
@@ -81,7 +82,7 @@ def main():
                     return hip.gemm_nt(x, w, c, 2, residual=rr, out=rr, split_k=sk)
                 return hip.gemm_nt(x, w, c, epi, split_k=sk)
 
-            cands = [(10, int(s)) for s in args.splits.split(",")]
+            cands = [(int(c), int(s)) for c in args.cfgs.split(",") for s in args.splits.split(",")]
             choice = plan.choose(M, N, K, epi)
             if choice is not None and choice[0] != 10:
                 cands.append(tuple(choice))
