@@ -62,7 +62,8 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20, help="timed windows")
     ap.add_argument("--warmup", type=int, default=5, help="untimed warmup windows")
-    ap.add_argument("--window-s", type=float, default=8.0, help="seconds per step (window)")
+    ap.add_argument("--window-s", type=float, default=12.0,
+                    help="seconds per step (window); 12 s x 20 steps = 240 s timed (VERDICT r3: resolvable headline)")
     ap.add_argument("--deadline-s", type=float, default=540.0,
                     help="stop timing early rather than run past this many seconds from process start")
     ap.add_argument("--model", default="qwen3-14b")
@@ -79,7 +80,7 @@ def parse(argv=None):
     ap.add_argument("--burnin-chars", default="320,420",
                     help="internal_strategy,public_reasoning characters of the burn-in outputs "
                          "(measured means of the engine's outputs: detail.age_mix.output_chars)")
-    ap.add_argument("--fill-max-s", type=float, default=200.0,
+    ap.add_argument("--fill-max-s", type=float, default=280.0,
                     help="wait (at most this long) until every game has finished its first decide "
                          "phase: the start-up prefill wave is over; the fill counts toward the warmup windows")
     ap.add_argument("--tp", type=int, default=1)
@@ -142,6 +143,7 @@ class SimPool:
         self.retired = 0          # accepted decisions of games already replaced
         self.games_finished = 0
         self.game_rounds = []     # rounds played by each finished game (burn-in rounds included)
+        self.engine_rounds = []   # ... of them on the engine (burn-in rounds excluded)
         self.ages = [0] * n_sims  # burn-in rounds of each slot's first game
         self.outcomes = {}
         self.errors = []
@@ -225,7 +227,9 @@ class SimPool:
                     with self.lock:
                         self.outcomes[o] = self.outcomes.get(o, 0) + 1
                         self.games_finished += 1
-                        self.game_rounds.append(min(sim.game.current_round, sim.game.max_rounds))
+                        played = min(sim.game.current_round, sim.game.max_rounds)
+                        self.game_rounds.append(played)
+                        self.engine_rounds.append(played - (self.ages[i] if self.generation[i] == 1 else 0))
                         self.retired += self._made(sim)
                         self.sims[i] = fresh
         except BaseException as exc:  # surfaced by the main thread
@@ -245,6 +249,25 @@ class SimPool:
     def check(self):
         if self.errors:
             raise self.errors[0]
+
+
+def window_stats(per_window, window_s: float):
+    """Spread of the per-window decision counts: the naive standard error of the mean window
+    (windows treated as independent) and the batch-means standard error over blocks of 4
+    windows (a game's phase completions cluster, so neighbouring windows anti-correlate and the
+    block estimate is the honest one for the run's total), both in % of the mean."""
+    import statistics
+    n = len(per_window)
+    if n < 2 or sum(per_window) == 0:
+        return {"n": n}
+    mean = statistics.fmean(per_window)
+    se = statistics.stdev(per_window) / n ** 0.5
+    out = {"n": n, "mean": round(mean, 1), "sd": round(statistics.stdev(per_window), 1),
+           "se_pct": round(100 * se / mean, 2)}
+    blocks = [sum(per_window[i:i + 4]) / 4 for i in range(0, n - n % 4, 4)]
+    if len(blocks) >= 2:
+        out["block4_se_pct"] = round(100 * statistics.stdev(blocks) / len(blocks) ** 0.5 / mean, 2)
+    return out
 
 
 def _heartbeat(llm, pool, stop: threading.Event, every: float = 30.0):
@@ -421,6 +444,18 @@ def main(argv=None):
         total_decisions = float(decisions)
     value = total_decisions / elapsed if elapsed > 0 else 0.0
     d_eng = {k: eng.get(k, 0) - stats0.get(k, 0) for k in eng}
+    # engine token rate of the timed region (uncached prompt + generated tokens), summed over DP
+    # replicas: the smooth companion of the bursty decision count (a game's 10 agents finish a
+    # phase together), used for A/B comparisons
+    tok = float(d_eng.get("prompt_tokens", 0) - d_eng.get("cached_tokens", 0) + d_eng.get("generated_tokens", 0))
+    if pool is None:
+        tok = 0.0  # TP followers: their driver counts the group's tokens
+    if world > 1:
+        tt = torch.tensor([tok], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM, group=ctrl)
+        tok = float(tt[0])
+    tokens_per_s = tok / elapsed if elapsed > 0 else 0.0
+    stats = window_stats(per_window, args.window_s)
     if rank == 0:
         line = {
             "metric": f"agent decisions/sec (node), {args.honest}h+{args.byzantine}b BCG {model.split('/')[-1]}; "
@@ -438,6 +473,7 @@ def main(argv=None):
                        "max_batch_seqs": C.ENGINE_CONFIG["max_batch_seqs"],
                        "max_tokens_decide": C.LLM_CONFIG["max_tokens_decide"],
                        "max_tokens_vote": C.LLM_CONFIG["max_tokens_vote"],
+                       "max_rounds": args.max_rounds, "age_p": args.age_p,
                        "step": f"{args.window_s:g} s window of the continuously-batched pool",
                        "parallelism": f"dp{world // args.tp}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
                        "hip_graphs": not args.no_graphs, "prefix_caching": not args.no_prefix_cache,
@@ -448,13 +484,22 @@ def main(argv=None):
                        "decisions_per_window_rank0": per_window,
                        "first5_vs_last5": [round(sum(per_window[:5]) / max(1, len(per_window[:5])), 1),
                                            round(sum(per_window[-5:]) / max(1, len(per_window[-5:])), 1)],
-                       "fill_s": round(fill_s, 1),
+                       "fill_s": round(fill_s, 1), "fill_max_s": args.fill_max_s,
+                       "fill_capped": fill_s >= args.fill_max_s - 0.5,
+                       "tokens_per_s": round(tokens_per_s, 1), "window_stats_rank0": stats,
                        "age_mix": {"p": args.age_p, "burnin_chars": args.burnin_chars,
                                    "mean_burnin_rounds": (round(sum(pool.ages) / len(pool.ages), 2)
                                                           if pool else None),
                                    "mean_rounds_per_finished_game": (
                                        round(sum(pool.game_rounds) / len(pool.game_rounds), 2)
                                        if pool and pool.game_rounds else None),
+                                   # rounds each finished game played on the engine (its burn-in
+                                   # rounds on the scripted CPU engine excluded)
+                                   "mean_engine_rounds_per_finished_game": (
+                                       round(sum(pool.engine_rounds) / len(pool.engine_rounds), 2)
+                                       if pool and pool.engine_rounds else None),
+                                   "protocol": ("burn-in (age-mixed pool, first games aged on a scripted "
+                                                "CPU engine)" if args.age_p > 0 else "fresh pool"),
                                    "output_chars": pool.output_chars() if pool else None},
                        "engine_per_rank": d_eng, "games_finished_rank0": pool.games_finished if pool else 0,
                        "outcomes_rank0": pool.outcomes if pool else {},

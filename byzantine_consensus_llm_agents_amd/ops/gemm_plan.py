@@ -93,6 +93,15 @@ class GemmPlan:
         cfg = self.default_cfg(M)
         return (cfg, 1) if self.supported(cfg, M, N, K, epi) else None
 
+    def _lookup(self, M: int, N: int, K: int, epi: int) -> Optional[Tuple[int, int]]:
+        """Table choice at M, else at the nearest measured M above (same projection shape)."""
+        choice = self.table.get((M, N, K, epi))
+        if choice is None and self.table:
+            above = [m for (m, n, k, e) in self.table if (n, k, e) == (N, K, epi) and m >= M]
+            if above:
+                choice = self.table[(min(above), N, K, epi)]
+        return choice
+
     def choose(self, M: int, N: int, K: int, epi: int) -> Optional[Tuple[int, int]]:
         """(tile configuration, split-K) of the hand kernel, or None for the library path."""
         if self.mode == "0":
@@ -105,11 +114,12 @@ class GemmPlan:
                     if self.supported(cfg, M, N, K, epi, split):
                         return (cfg, split)
             return None
-        choice = self.table.get((M, N, K, epi))
-        if choice is None and self.table:  # nearest measured M above (same projection shape)
-            above = [m for (m, n, k, e) in self.table if (n, k, e) == (N, K, epi) and m >= M]
-            if above:
-                choice = self.table[(min(above), N, K, epi)]
+        choice = self._lookup(M, N, K, epi)
+        if choice is None and epi in (0, 2):
+            # the store and residual epilogues run the same tile loop: a shape measured with one
+            # (e.g. the TP row-parallel o / down projections, tuned with the residual epilogue
+            # but called with the store epilogue before the fused all-reduce) takes that choice
+            choice = self._lookup(M, N, K, 2 - epi)
         if choice is not None:
             return choice if choice[0] >= 0 and self.supported(choice[0], M, N, K, epi, choice[1]) else None
         if M > self.max_m or self.table:  # a measured table exists: unlisted shapes stay on the library

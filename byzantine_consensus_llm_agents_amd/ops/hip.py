@@ -215,14 +215,27 @@ def hip_ops() -> SimpleNamespace:
             4, _kv_fp8(k_cache, v_cache), _stream()), "paged_attention_prefill")
         return out
 
-    def linear(x, w, bias=None):
+    # Per-call GEMM dispatch log (which projection shapes reach a hand kernel, also
+    # inside TP worker processes that no profiler sees): (M, N, K, epi, dtype) -> choice -> calls.
+    # Off unless enabled (BCG_GEMM_LOG=1 or dispatch_log.enable()); graph-captured calls are
+    # logged once, at capture (the replays run the same kernels).
+    dispatch_log = SimpleNamespace(enabled=os.environ.get("BCG_GEMM_LOG") == "1", calls={})
+
+    def _log(M, N, K, epi, choice, dtype="bf16"):
+        if dispatch_log.enabled:
+            key = (M, N, K, epi, dtype, "lib" if choice is None else f"{choice[0]}x{choice[1]}")
+            dispatch_log.calls[key] = dispatch_log.calls.get(key, 0) + 1
+
+    def linear(x, w, bias=None, _epi_log=0):
         """y = x W^T (+b): hand MFMA GEMM where the plan says it beats hipBLASLt, hipBLASLt otherwise."""
         M, K = x.shape
         N = w.shape[0]
+        cfg = None
         if x.is_contiguous() and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
             cfg = plan.choose(M, N, K, 0)
-            if cfg is not None:
-                return gemm_nt(x, w, cfg, 0, bias=bias)
+        _log(M, N, K, _epi_log, cfg)
+        if cfg is not None:
+            return gemm_nt(x, w, cfg, 0, bias=bias)
         return torch.nn.functional.linear(x, w, bias)
 
     from .gemm_plan import PP_CFG, GemmPlan
@@ -305,7 +318,8 @@ def hip_ops() -> SimpleNamespace:
         M, K = x.shape
         cfg = plan.choose(M, w.shape[0], K, 1) if x.is_contiguous() and x.dtype == torch.bfloat16 else None
         if cfg is None:
-            return silu_mul(linear(x, w))
+            return silu_mul(linear(x, w, _epi_log=1))
+        _log(M, w.shape[0], K, 1, cfg)
         return gemm_nt(x, w, cfg, 1)
 
     residual_addmm = os.environ.get("BCG_RESIDUAL_ADDMM", "1") == "1"
@@ -315,13 +329,14 @@ def hip_ops() -> SimpleNamespace:
         residual-stream update of the next add+RMSNorm).  Returns `residual`."""
         M, K = x.shape
         cfg = plan.choose(M, w.shape[0], K, 2) if x.is_contiguous() and x.dtype == torch.bfloat16 else None
+        _log(M, w.shape[0], K, 2, cfg)
         if cfg is None:
             if (residual_addmm and residual.is_contiguous() and residual.dtype == x.dtype == w.dtype
                     and residual.shape == (M, w.shape[0])):
                 # hipBLASLt with beta = 1: the residual add rides in the GEMM epilogue (one read
                 # of the residual, no separate elementwise pass over three [M, H] tensors)
                 return residual.addmm_(x, w.t())
-            residual.add_(linear(x, w))
+            residual.add_(torch.nn.functional.linear(x, w))
             return residual
         return gemm_nt(x, w, cfg, 2, residual=residual, out=residual)
 
@@ -444,10 +459,12 @@ def hip_ops() -> SimpleNamespace:
         """fp8 projection with row-wise activation and per-channel weight scales: the hand
         fp8 MFMA kernel for decode-sized M, hipBLASLt (torch._scaled_mm) otherwise."""
         _req(xq.dtype == f8 and wq.dtype == f8 and xq.shape[1] == wq.shape[1], "linear_fp8 operands")
+        cfg = None
         if out_dtype == torch.bfloat16 and xq.is_contiguous() and wq.is_contiguous():
             cfg = fp8_cfg(xq.shape[0], wq.shape[0], xq.shape[1])
-            if cfg is not None:
-                return gemm_nt_fp8(xq, xs.contiguous(), wq, ws.contiguous(), cfg, 0, bias=bias)
+        _log(xq.shape[0], wq.shape[0], xq.shape[1], 0, cfg, "fp8")
+        if cfg is not None:
+            return gemm_nt_fp8(xq, xs.contiguous(), wq, ws.contiguous(), cfg, 0, bias=bias)
         return torch._scaled_mm(xq, wq.t(), scale_a=xs.view(-1, 1), scale_b=ws.view(1, -1), bias=bias,
                                 out_dtype=out_dtype)
 
@@ -473,5 +490,5 @@ def hip_ops() -> SimpleNamespace:
                            paged_attention_decode=paged_attention_decode,
                            decode_workspace_numel=decode_workspace_numel,
                            paged_attention_prefill=paged_attention_prefill,
-                           sample_step=sample_step,
+                           sample_step=sample_step, dispatch_log=dispatch_log,
                            library=lib)

@@ -43,25 +43,58 @@
 #ifndef W4_GROUP_M
 #define W4_GROUP_M 8  // m-tiles per tile-order group (L2 reuse of both operands)
 #endif
-// schedule knobs: first MFMA slot and slot stride of each memory-op stream (64 slots/phase)
+#ifndef W4_MFMA32
+#define W4_MFMA32 0  // 1: v_mfma_f32_32x32x16_bf16 (32 MFMAs per phase) instead of 16x16x32 (64)
+#endif
+// schedule knobs: first MFMA slot and slot stride of each memory-op stream (W4_SLOTS per phase)
+#if W4_MFMA32
+#define W4_SLOTS 32
+#else
+#define W4_SLOTS 64
+#endif
+// Defaults (measured, profiles/r4_gemm_w4/): the five-slot ring; phase A: the 16 k-step-1
+// reads in its first half, X(t+2)'s 8 pieces in its second; phase B: W(t+2)'s 8 pieces every
+// 8th slot, the 16 next-tile reads every 4th.
+#ifndef W4_RING5
+#define W4_RING5 1  // 1: five 32-KiB LDS slots, X(t+2) loaded in phase A(t), W(t+2) in phase B(t); 0: two stages
+#endif
 #ifndef W4_RA0
 #define W4_RA0 0  // phase A: k-step-1 reads
 #endif
 #ifndef W4_RAS
-#define W4_RAS 2
+#define W4_RAS (W4_SLOTS / 32)
+#endif
+#ifndef W4_DA0
+#define W4_DA0 (W4_SLOTS / 2 + 1)  // RING5 phase A: LDS-DMA pieces of X(t+2)
+#endif
+#ifndef W4_DAS
+#define W4_DAS (W4_SLOTS / 16)
 #endif
 #ifndef W4_DB0
 #define W4_DB0 0  // phase B: LDS-DMA pieces
 #endif
 #ifndef W4_DBS
-#define W4_DBS 3
+#define W4_DBS (W4_RING5 ? W4_SLOTS / 8 : W4_SLOTS / 16)
 #endif
 #ifndef W4_RB0
-#define W4_RB0 1  // phase B: k-step-0 reads of the next tile
+#define W4_RB0 (W4_SLOTS / 32)  // phase B: k-step-0 reads of the next tile
 #endif
 #ifndef W4_RBS
-#define W4_RBS 3
+#define W4_RBS (W4_SLOTS / 16)
 #endif
+// timing ablations only (wrong results): pieces issued in phase B, and the first piece index
+#ifndef W4_ABL_NPIECE
+#define W4_ABL_NPIECE 16
+#endif
+#ifndef W4_ABL_PIECE0
+#define W4_ABL_PIECE0 0
+#endif
+#define W4_NPB (W4_RING5 ? 8 : W4_ABL_NPIECE)  // pieces issued in phase B
+#ifndef W4_M0_EARLY
+#define W4_M0_EARLY 0  // 1: each piece's M0 write one MFMA ahead of the piece (needs W4_DB0 >= 1)
+#endif
+static_assert(!W4_M0_EARLY || W4_DB0 >= 1, "M0 is written one slot before the first piece");
+static_assert(!W4_RING5 || (W4_DA0 + 7 * W4_DAS < W4_SLOTS && !W4_M0_EARLY), "RING5 schedule");
 
 namespace {
 
@@ -71,8 +104,10 @@ enum Epilogue { EPI_STORE = 0, EPI_SILU_MUL = 1, EPI_RESIDUAL = 2 };
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-static_assert(W4_RA0 + 15 * W4_RAS < 64 && W4_DB0 + 15 * W4_DBS < 64 && W4_RB0 + 15 * W4_RBS < 64,
+static_assert(W4_RA0 + 15 * W4_RAS < W4_SLOTS && W4_DB0 + (W4_NPB - 1) * W4_DBS < W4_SLOTS &&
+                  W4_RB0 + 15 * W4_RBS < W4_SLOTS,
               "each stream fits its phase");
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
 
@@ -97,14 +132,22 @@ __device__ __forceinline__ i32x4 make_srd(const void* base, uint32_t bytes) {
 __device__ uint64_t w4_stamps[1 << 16];  // [workgroup][wave][phase A, wait, phase B, K-tiles]
 #endif
 
-template <int EPI>
+template <int EPI, bool M32>
 __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_w4_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ W, const bf16_t* __restrict__ bias,
     const bf16_t* __restrict__ residual, bf16_t* __restrict__ C, float* __restrict__ ws,
     int* __restrict__ counters, int M, int N, int K, int ldc, int inter, int m_tiles, int n_tiles,
     int split_k) {
   // ONE shared array (cdna_hip_programming.md "Projection GEMM" item 4a)
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE];
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[W4_RING5 ? 5 * A_BYTES : 2 * STAGE];
+  // LDS byte offset of tile t's X (part 0) or W (part 1) half: two 64-KiB stages, or (RING5) a
+  // ring of five 32-KiB slots, tile t in slots 2t, 2t+1 (mod 5)
+  auto slot_off = [](int t, int part) -> uint32_t {
+    if constexpr (W4_RING5)
+      return static_cast<uint32_t>((2 * t + part) % 5) * A_BYTES;
+    else
+      return static_cast<uint32_t>(t & 1) * STAGE + part * A_BYTES;
+  };
 
   // ---- XCD-aware order (bijective remap), grouped m-tiles, then (tile, k-split) ----
   const int nwg = m_tiles * n_tiles * split_k;
@@ -149,13 +192,23 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   for (int i = 0; i < 8; ++i) vX[i] = voffX + i * strideX, vW[i] = voffW + i * strideW;
   const uint32_t lds_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem));
   // piece q (0..15) of tile t into `stage`: q < 8 X piece q, else W piece q - 8
-  auto dma = [&](int t, int stage, int q, const i32x4& sX, const i32x4& sW) {
+  auto dma_m0 = [&](int t, int q) {
+    return __builtin_amdgcn_readfirstlane(lds_base + slot_off(t, q >= 8) + (q & 7) * 4096 + wave * 1024);
+  };
+  // mode 0: M0 write + piece in one statement; 1: the piece only (M0 set earlier: set_m0)
+  auto dma = [&](int t, int q, const i32x4& sX, const i32x4& sW, int mode = 0) {
     const uint32_t kb = static_cast<uint32_t>(kt0 + t) * (BK * 2);
     const bool isx = q < 8;
     const int i = q & 7;
     const uint32_t soff = __builtin_amdgcn_readfirstlane(kb);
-    const uint32_t m0v = __builtin_amdgcn_readfirstlane(lds_base + stage * STAGE + (isx ? 0 : A_BYTES) +
-                                                        i * 4096 + wave * 1024);
+    if (mode == 1) {
+      if (isx)
+        asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(vX[i]), "s"(sX), "s"(soff) : "memory");
+      else
+        asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(vW[i]), "s"(sW), "s"(soff) : "memory");
+      return;
+    }
+    const uint32_t m0v = dma_m0(t, q);
     if (isx) {
       asm volatile("s_mov_b32 m0, %3\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
                    :
@@ -168,13 +221,26 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
                    : "memory", "m0");
     }
   };
+  auto set_m0 = [&](int t, int q) {
+    asm volatile("s_mov_b32 m0, %0" : : "s"(dma_m0(t, q)) : "memory", "m0");
+  };
 
-  // ---- fragments of a 32-deep k-step: x block f = stage row wm*128 + 16 f + fr, w block f =
-  // stage row A_BYTES/128 + wn*128 + 16 f + fr; chunk 4 s + fq, swizzled by (fr >> 1) & 7
-  const int rd_sw = (fr >> 1) & 7;
-  const int rdA = (wm * 128 + fr) * 128, rdB = A_BYTES + (wn * 128 + fr) * 128;
-  auto read_frag = [&](int stage, int s, int f, bf16x8 (&xf)[8], bf16x8 (&wf)[8]) {
-    const int off = stage * STAGE + (((4 * s + fq) ^ rd_sw) << 4) + (f & 7) * 2048 + (f < 8 ? rdA : rdB);
+  // ---- fragments of one phase (32 of the K-tile's 64; half s = 0: chunks 0-3, 1: chunks 4-7):
+  //   16x16x32: block f < 8 = X rows wm*128 + 16 f + fr, f >= 8 = W rows wn*128 + 16 (f-8) + fr,
+  //             chunk 4 s + fq;  lane -> swizzle (fr >> 1) & 7
+  //   32x32x16: f < 8 = X k-step f >> 2 (16 deep), rows wm*128 + 32 (f & 3) + (lane & 31);
+  //             f >= 8 = the same for W;  chunk 4 s + 2 ks + (lane >> 5); swizzle ((lane & 31) >> 1) & 7
+  const int r_lane = M32 ? (lane & 31) : fr;
+  const int rd_sw = (r_lane >> 1) & 7;
+  const int rdA = (wm * 128 + r_lane) * 128, rdB = (wn * 128 + r_lane) * 128;
+  auto read_frag = [&](int t, int s, int f, bf16x8 (&xf)[8], bf16x8 (&wf)[8]) {
+    int off = slot_off(t, f >= 8) + (f < 8 ? rdA : rdB);
+    if constexpr (M32) {
+      const int ks = (f >> 2) & 1, blk = f & 3;
+      off += (((4 * s + 2 * ks + (lane >> 5)) ^ rd_sw) << 4) + blk * 4096;
+    } else {
+      off += (((4 * s + fq) ^ rd_sw) << 4) + (f & 7) * 2048;
+    }
     const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + off);
     if (f < 8)
       xf[f] = v;
@@ -182,39 +248,50 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       wf[f - 8] = v;
   };
 
-  f32x4 acc[8][8];  // [n-block][m-block], pinned in AGPRs by the asm MFMA below
+  // accumulators, pinned in AGPRs by the asm MFMA below: [n-block][m-block]
+  using Acc = std::conditional_t<M32, f32x16[4][4], f32x4[8][8]>;
+  constexpr int NB = M32 ? 4 : 8;
+  Acc acc;
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < NB; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NB; ++j) acc[i][j] = 0.f;
   // "memory" keeps the MFMAs in source order with the LDS reads and DMA issued between them;
   // the builtin form lets hipcc cycle the accumulators through a few AGPRs (gemm_rs.hip)
   auto mf = [&](int idx, const bf16x8 (&xf)[8], const bf16x8 (&wf)[8]) {
-    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
-                 : "+a"(acc[idx >> 3][idx & 7])
-                 : "v"(wf[idx >> 3]), "v"(xf[idx & 7])
-                 : "memory");
+    if constexpr (M32) {  // idx = ks * 16 + nb * 4 + mb
+      const int ks = idx >> 4, nb = (idx >> 2) & 3, mb = idx & 3;
+      asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0"
+                   : "+a"(acc[nb][mb])
+                   : "v"(wf[ks * 4 + nb]), "v"(xf[ks * 4 + mb])
+                   : "memory");
+    } else {
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                   : "+a"(acc[idx >> 3][idx & 7])
+                   : "v"(wf[idx >> 3]), "v"(xf[idx & 7])
+                   : "memory");
+    }
   };
 
   bf16x8 x0[8], w0[8], x1[8], w1[8];
   // ---- prologue: tiles 0 and 1 in flight, tile 0 landed, k-step 0 of tile 0 in registers ----
 #pragma unroll
-  for (int q = 0; q < 16; ++q) dma(0, 0, q, srdX, srdW);
+  for (int q = 0; q < 16; ++q) dma(0, q, srdX, srdW);
   if (nk > 1) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) dma(1, 1, q, srdX, srdW);
+    for (int q = 0; q < 16; ++q) dma(1, q, srdX, srdW);
     asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
 #pragma unroll
   for (int f = 0; f < 16; ++f) read_frag(0, 0, f, x0, w0);
+  i32x4 nullX = srdX, nullW = srdW;  // zero-range descriptors: pieces past the last tile
+  nullX[2] = 0, nullW[2] = 0;
 
   // phase B of tile t.  Past the last tile the pieces go through a zero-range descriptor: no
   // memory traffic, the zeros land in a stage nobody reads -- branch-free, one body (a
   // branch around the pieces, or two copies of the phase, made hipcc spill the accumulators)
-  i32x4 nullX = srdX, nullW = srdW;
-  nullX[2] = 0, nullW[2] = 0;
   auto phase_b = [&](int t, int cur) {
     const bool more = t + 2 < nk;
     i32x4 sX, sW;
@@ -223,15 +300,19 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       sX[e] = __builtin_amdgcn_readfirstlane(more ? srdX[e] : nullX[e]),
       sW[e] = __builtin_amdgcn_readfirstlane(more ? srdW[e] : nullW[e]);
 #pragma clang loop unroll(full)
-    for (int idx = 0; idx < 64; ++idx) {
+    for (int idx = 0; idx < W4_SLOTS; ++idx) {
       mf(idx, x1, w1);
 #ifndef W4_ABL_NODMA
-      if (idx >= W4_DB0 && (idx - W4_DB0) % W4_DBS == 0 && (idx - W4_DB0) / W4_DBS < 16)
-        dma(t + 2, cur, (idx - W4_DB0) / W4_DBS, sX, sW);
+#if W4_M0_EARLY  // M0 written one MFMA before its piece (W4_DB0 >= 1)
+      if (idx + 1 >= W4_DB0 && (idx + 1 - W4_DB0) % W4_DBS == 0 && (idx + 1 - W4_DB0) / W4_DBS < W4_NPB)
+        set_m0(t + 2, (idx + 1 - W4_DB0) / W4_DBS + W4_ABL_PIECE0 + (W4_RING5 ? 8 : 0));
+#endif
+      if (idx >= W4_DB0 && (idx - W4_DB0) % W4_DBS == 0 && (idx - W4_DB0) / W4_DBS < W4_NPB)
+        dma(t + 2, (idx - W4_DB0) / W4_DBS + W4_ABL_PIECE0 + (W4_RING5 ? 8 : 0), sX, sW, W4_M0_EARLY);
 #endif
 #ifndef W4_ABL_NOREAD
       if (idx >= W4_RB0 && (idx - W4_RB0) % W4_RBS == 0 && (idx - W4_RB0) / W4_RBS < 16)
-        read_frag(cur ^ 1, 0, (idx - W4_RB0) / W4_RBS, x0, w0);  // tile t+1 (garbage after the last)
+        read_frag(t + 1, 0, (idx - W4_RB0) / W4_RBS, x0, w0);  // tile t+1 (garbage after the last)
 #endif
     }
   };
@@ -240,18 +321,35 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 #endif
   for (int t = 0; t < nk; ++t) {
     const int cur = t & 1;
+#if W4_RING5
+    const bool more_a = t + 2 < nk;
+    i32x4 aX;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) aX[e] = __builtin_amdgcn_readfirstlane(more_a ? srdX[e] : nullX[e]);
+#endif
 #pragma clang loop unroll(full)
-    for (int idx = 0; idx < 64; ++idx) {  // phase A
+    for (int idx = 0; idx < W4_SLOTS; ++idx) {  // phase A
       mf(idx, x0, w0);
+#if W4_RING5  // X(t+2) into the slot W(t-1) left (free since the barrier of tile t-1)
+      if (idx >= W4_DA0 && (idx - W4_DA0) % W4_DAS == 0 && (idx - W4_DA0) / W4_DAS < 8)
+        dma(t + 2, (idx - W4_DA0) / W4_DAS, aX, aX);
+#endif
+#ifdef W4_ABL_SPREAD  // timing ablation (racy): pieces 0..7 of tile t+2 issued in phase A
+      if (idx % (W4_SLOTS / 8) == 2) dma(t + 2, idx / (W4_SLOTS / 8), srdX, srdW);
+#endif
 #ifndef W4_ABL_NOREAD
       if (idx >= W4_RA0 && (idx - W4_RA0) % W4_RAS == 0 && (idx - W4_RA0) / W4_RAS < 16)
-        read_frag(cur, 1, (idx - W4_RA0) / W4_RAS, x1, w1);
+        read_frag(t, 1, (idx - W4_RA0) / W4_RAS, x1, w1);
 #endif
     }
 #ifdef W4_STAMPS
     const uint64_t t_a = __builtin_amdgcn_s_memtime();
 #endif
+#if W4_RING5  // tile t+1 landed; X(t+2)'s 8 pieces of this phase may stay in flight
+    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
 #ifdef W4_STAMPS
     const uint64_t t_w = __builtin_amdgcn_s_memtime();
     cyc_a += t_a - t_end, cyc_w += t_w - t_a;
@@ -272,37 +370,58 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   // the last MFMAs' results are read by VALU / stores below: cover the MFMA D -> read hazard
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
 
-  // ---- epilogue: lane holds D[n = 4fq + e][m = fr] of block (i, j), value(i, j) ----
+  // ---- epilogue.  The tile is seen as [n-group][m-block] quads of 4 consecutive output columns
+  // (n) of one row (m) per lane: q = quad(i, j) with i over 32 n-groups, j over NB m-blocks.
+  //   16x16x32: block (nb, mb) lane: D[n = 16 nb + 4 fq + e][m = 16 mb + fr];  i = nb
+  //   32x32x16: block (nb, mb) lane: D[n = 32 nb + 8 g + 4 (lane >> 5) + e][m = 32 mb + (lane & 31)],
+  //             registers 4 g + e;  i = 4 nb + g (g = 0..3)
+  // value(nb, mb) returns the block's registers (accumulators, or the split-K slab sum).
   auto epilogue = [&](auto value) {
+    constexpr int MB = M32 ? 32 : 16;
+    const int ml = M32 ? (lane & 31) : fr;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int m = m0 + wm * 128 + j * 16 + fr;
+    for (int j = 0; j < NB; ++j) {
+      const int m = m0 + wm * 128 + j * MB + ml;
       if (m >= M) continue;
-      if constexpr (EPI == EPI_SILU_MUL) {
 #pragma unroll
-        for (int i = 0; i < 8; i += 2) {  // (gate, up) block pairs of the same 16 features
-          const int feat = (n0 >> 1) + wn * 64 + (i >> 1) * 16 + 4 * fq;
-          const f32x4 g = value(i, j), u = value(i + 1, j);
-          *reinterpret_cast<u16x4*>(C + static_cast<size_t>(m) * ldc + feat) =
-              pack4(silu(g[0]) * u[0], silu(g[1]) * u[1], silu(g[2]) * u[2], silu(g[3]) * u[3]);
-        }
-      } else {
+      for (int nb = 0; nb < NB; ++nb) {
+        const auto blk = value(nb, j);
+        constexpr int NG = M32 ? 4 : 1;  // quads per block
+        if constexpr (EPI == EPI_SILU_MUL) {
+          // 16-row blocks of the tile alternate gate / up of the same 16 features:
+          //   16x16x32: block pairs (nb, nb+1);  32x32x16: quads g and g + 2 of one block
+          if constexpr (M32) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int n = n0 + wn * 128 + i * 16 + 4 * fq;
-          if (n >= N) continue;
-          f32x4 v = value(i, j);
-          if (bias != nullptr) {
-            const u16x4 b = *reinterpret_cast<const u16x4*>(bias + n);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += bf2f(b[e]);
+            for (int g = 0; g < 2; ++g) {
+              const int feat = (n0 >> 1) + wn * 64 + nb * 16 + 8 * g + 4 * (lane >> 5);
+              *reinterpret_cast<u16x4*>(C + static_cast<size_t>(m) * ldc + feat) =
+                  pack4(silu(blk[4 * g]) * blk[4 * g + 8], silu(blk[4 * g + 1]) * blk[4 * g + 9],
+                        silu(blk[4 * g + 2]) * blk[4 * g + 10], silu(blk[4 * g + 3]) * blk[4 * g + 11]);
+            }
+          } else if (nb % 2 == 0) {
+            const auto u = value(nb + 1, j);
+            const int feat = (n0 >> 1) + wn * 64 + (nb >> 1) * 16 + 4 * fq;
+            *reinterpret_cast<u16x4*>(C + static_cast<size_t>(m) * ldc + feat) =
+                pack4(silu(blk[0]) * u[0], silu(blk[1]) * u[1], silu(blk[2]) * u[2], silu(blk[3]) * u[3]);
           }
-          if constexpr (EPI == EPI_RESIDUAL) {
-            const u16x4 rr = *reinterpret_cast<const u16x4*>(residual + static_cast<size_t>(m) * ldc + n);
+        } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += bf2f(rr[e]);
+          for (int g = 0; g < NG; ++g) {
+            const int n = n0 + wn * 128 + (M32 ? nb * 32 + 8 * g + 4 * (lane >> 5) : nb * 16 + 4 * fq);
+            if (n >= N) continue;
+            float v[4] = {blk[4 * g], blk[4 * g + 1], blk[4 * g + 2], blk[4 * g + 3]};
+            if (bias != nullptr) {
+              const u16x4 b = *reinterpret_cast<const u16x4*>(bias + n);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] += bf2f(b[e]);
+            }
+            if constexpr (EPI == EPI_RESIDUAL) {
+              const u16x4 rr = *reinterpret_cast<const u16x4*>(residual + static_cast<size_t>(m) * ldc + n);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] += bf2f(rr[e]);
+            }
+            *reinterpret_cast<u16x4*>(C + static_cast<size_t>(m) * ldc + n) = pack4(v[0], v[1], v[2], v[3]);
           }
-          *reinterpret_cast<u16x4*>(C + static_cast<size_t>(m) * ldc + n) = pack4(v[0], v[1], v[2], v[3]);
         }
       }
     }
@@ -314,18 +433,26 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   }
   // ---- split-K: every split stores its fp32 tile write-through (sc1); the last arriver sums
   // all the slabs (its own included) straight into the epilogue -- the accumulators die at
-  // the store, so the reduction needs no second register copy of the tile
+  // the store, so the reduction needs no second register copy of the tile.  Slab layout: per
+  // (wave, block, 16-B quarter) 256 floats, lane-major (any layout both sides agree on).
+  constexpr int QPB = M32 ? 4 : 1;  // 16-B quarters per block per lane
   float* slab = ws + static_cast<size_t>(tile) * split_k * (BM * BN);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, split_k * BM * BN * 4, 0x00020000);
   __syncthreads();  // every wave is past its last ds_read: smem is reusable as the flag slot
   int* flag = reinterpret_cast<int*>(smem);
+  auto slab_off = [&](int sp, int i, int j, int qq) {
+    return (sp * (BM * BN) + (((wave * NB + i) * NB + j) * QPB + qq) * 256 + lane * 4) * 4;
+  };
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < NB; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int off = (split * (BM * BN) + ((wave * 8 + i) * 8 + j) * 256 + lane * 4) * 4;
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, off, 0, 16 /*sc1*/);
-    }
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int qq = 0; qq < QPB; ++qq) {
+        const f32x4 part = {acc[i][j][4 * qq], acc[i][j][4 * qq + 1], acc[i][j][4 * qq + 2], acc[i][j][4 * qq + 3]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, part), rs, slab_off(split, i, j, qq), 0,
+                                               16 /*sc1*/);
+      }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
@@ -338,11 +465,15 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   if (!flag[0]) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   epilogue([&](int i, int j) {
-    f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int sp = 0; sp < split_k; ++sp) {
-      const int off = (sp * (BM * BN) + ((wave * 8 + i) * 8 + j) * 256 + lane * 4) * 4;
-      sum += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16 /*sc1*/));
-    }
+    std::remove_reference_t<decltype(acc[0][0])> sum = 0.f;
+    for (int sp = 0; sp < split_k; ++sp)
+#pragma unroll
+      for (int qq = 0; qq < QPB; ++qq) {
+        const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, slab_off(sp, i, j, qq), 0,
+                                                                                        16 /*sc1*/));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sum[4 * qq + e] += v[e];
+      }
     return sum;
   });
 }
@@ -352,7 +483,7 @@ int launch_w4(const void* x, const void* w, const void* bias, const void* res, v
               int N, int K, int inter, int split_k, hipStream_t stream) {
   const int m_tiles = (M + BM - 1) / BM, n_tiles = (N + BN - 1) / BN;
   const int ldc = EPI == EPI_SILU_MUL ? inter : N;
-  hipLaunchKernelGGL((gemm_w4_kernel<EPI>), dim3(m_tiles * n_tiles * split_k), dim3(256), 0, stream,
+  hipLaunchKernelGGL((gemm_w4_kernel<EPI, W4_MFMA32 != 0>), dim3(m_tiles * n_tiles * split_k), dim3(256), 0, stream,
                      static_cast<const bf16_t*>(x), static_cast<const bf16_t*>(w), static_cast<const bf16_t*>(bias),
                      static_cast<const bf16_t*>(res), static_cast<bf16_t*>(c), ws, cnt, M, N, K, ldc, inter, m_tiles,
                      n_tiles, split_k);

@@ -76,3 +76,21 @@ def test_bench_tp2_torch_engine_continuous_batching():
                 "--steps", "2", "--warmup", "1", "--window-s", "4"], timeout=600)
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp1xtp2" and out["steps"] == 2
     assert out["detail"]["engine_per_rank"]["decode_steps"] > 0
+
+
+def test_bench_reports_resolution_fields():
+    """tokens/s and the window spread are in detail, max_rounds in config."""
+    out = _run(["--steps", "4", "--warmup", "1", "--max-rounds", "7"])
+    d = out["detail"]
+    assert out["config"]["max_rounds"] == 7
+    assert {"tokens_per_s", "window_stats_rank0", "fill_max_s", "fill_capped"} <= set(d)
+    assert d["window_stats_rank0"]["n"] == 4
+    assert "protocol" in d["age_mix"]
+
+
+def test_window_stats_block_estimate():
+    sys.path.insert(0, ROOT)
+    from bench import window_stats
+    s = window_stats([100, 300] * 4, 12.0)  # perfectly anti-correlated neighbours
+    assert s["se_pct"] > 10 and s["block4_se_pct"] == 0.0
+    assert window_stats([5], 12.0) == {"n": 1}

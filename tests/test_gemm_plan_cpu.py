@@ -69,3 +69,17 @@ def test_fp8_plan_table_rule_and_library(tmp_path, monkeypatch):
     monkeypatch.setenv("BCG_HAND_GEMM", "1")
     shipped = Fp8Plan(tiles, FP8_TABLE)            # the shipped Mistral-22B table loads and is usable
     assert shipped.table and shipped.choose(160, 8192, 6144) is not None
+
+
+def test_store_epilogue_takes_residual_table_entry():
+    """TP row-parallel o / down projections are called with the store epilogue (the residual
+    add rides in the fused all-reduce) but the table measured them with the residual epilogue:
+    the same tile loop, so the plan takes that choice."""
+    from byzantine_consensus_llm_agents_amd.ops.gemm_plan import GemmPlan
+    plan = GemmPlan()
+    for M in (16, 256, 704):
+        for N, K in ((5120, 2048), (5120, 6400)):  # Qwen3-32B TP=4 o / down shards
+            assert plan._lookup(M, N, K, 0) is None and plan._lookup(M, N, K, 2) is not None
+            got = plan.choose(M, N, K, 0)
+            want = plan.choose(M, N, K, 2)
+            assert got == want
