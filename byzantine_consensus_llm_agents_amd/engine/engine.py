@@ -155,7 +155,7 @@ class InferenceEngine:
         if self.backend == "hip" and not torch.cuda.is_available():
             raise RuntimeError("hip backend requested but no GPU is visible")
         # TP first: joining the process group selects this rank's GPU (LOCAL_RANK)
-        self.tp = self._init_tp(args.tensor_parallel_size)
+        self.tp = self._init_tp(args.tensor_parallel_size, cfg.hidden_size)
         if args.device:
             self.device = torch.device(args.device)
         elif self.backend == "hip":
@@ -227,12 +227,12 @@ class InferenceEngine:
             self.graphs = DecodeGraphs(self)
 
     # ------------------------------------------------------------- setup
-    def _init_tp(self, tp_size: int) -> TPGroup:
+    def _init_tp(self, tp_size: int, hidden: int) -> TPGroup:
         if tp_size <= 1:
             return TPGroup()
         from ..parallel.groups import tensor_parallel_group
         return tensor_parallel_group(tp_size, custom_allreduce=(
-            self.backend == "hip" and ENGINE_CONFIG.get("custom_allreduce", True)))
+            self.backend == "hip" and ENGINE_CONFIG.get("custom_allreduce", True)), hidden=hidden)
 
     def kv_dtype(self) -> torch.dtype:
         kd = (self.args.kv_cache_dtype or "auto").lower()

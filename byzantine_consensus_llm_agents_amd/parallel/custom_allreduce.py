@@ -28,6 +28,7 @@ import torch
 
 ONESHOT_MAX = 1 << 20          # bytes: one-shot below, two-shot above
 DEFAULT_CAP = 32 << 20         # bytes per message handled by the custom kernels
+DECODE_FLOOR = 8 << 20         # bytes: messages this small always stay on the kernels (decode graphs)
 THREADS = 512
 
 
@@ -43,9 +44,10 @@ def pick_thresholds(sizes: List[int], t_one: List[float], t_two: List[float], t_
 
     Returns ``(oneshot_limit, route_max)``: one-shot up to the largest measured size at which it
     still beats two-shot (0: two-shot from the smallest size on), the custom kernels up to the
-    largest measured size at which the better of them beats RCCL (RCCL beyond; ``cap_bytes`` when
-    they win everywhere).  Both limits are measured sizes (no extrapolation), and only a prefix
-    of wins counts: above the first size where a method loses, the other one is used.
+    largest measured size at which the kernel the routing actually picks there (one-shot up to
+    ``oneshot_limit``, two-shot above) beats RCCL (RCCL beyond; ``cap_bytes`` when it wins
+    everywhere).  Both limits are measured sizes (no extrapolation), and only a prefix of wins
+    counts: above the first size where a method loses, the other one is used.
     """
     oneshot_limit = 0
     for nb, a, b in zip(sizes, t_one, t_two):
@@ -54,7 +56,7 @@ def pick_thresholds(sizes: List[int], t_one: List[float], t_two: List[float], t_
         oneshot_limit = nb
     route_max = 0
     for nb, a, b, r in zip(sizes, t_one, t_two, t_rccl):
-        if min(a, b) > r:
+        if (a if nb <= oneshot_limit else b) > r:
             break
         route_max = nb
     if route_max == sizes[-1]:
@@ -88,7 +90,7 @@ def _lib():
            "bcg_ar_set_error": [vp],
            "bcg_ar_allreduce": [P, P, c_int, c_int, vp, vp, c_int64, c_int64, c_int, c_int, c_double, vp],
            "bcg_ar_allreduce_addnorm": [P, P, c_int, c_int, vp, vp, vp, vp, c_int, c_int, ctypes.c_float,
-                                        c_int64, c_int, c_double, vp]}
+                                        c_int64, c_int, c_double, c_int, vp]}
     for name, argtypes in sig.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
@@ -113,6 +115,7 @@ class _Rank:
         self.calls = {1: 0, 2: 0}
         self.route_max = cap_bytes   # messages routed to the kernels (RCCL above); calibrate() may lower it
         self.oneshot_limit = None    # measured one-shot limit (None: the choose_mode rule)
+        self.addnorm_oneshot_limit = None  # ... of the fused all-reduce + add + RMSNorm kernels
         self.calibration = None
 
     def can(self, x: torch.Tensor) -> bool:
@@ -142,21 +145,34 @@ class _Rank:
         self.calls[mode] += 1
         return out
 
-    def calibrate(self, group, sizes: Optional[List[int]] = None, iters: int = 20, route: bool = True) -> dict:
+    def calibrate(self, group, sizes: Optional[List[int]] = None, iters: int = 20, route: bool = True,
+                  hidden: Optional[int] = None) -> dict:
         """Measure one-shot, two-shot and RCCL (``dist.all_reduce`` on `group`) on this group's
         own links at a few message sizes and set the routing limits from the table
         (``pick_thresholds``).  Collective over the group; the timings are max-reduced first, so
         every rank routes identically.  Replaces the built-in guesses (``ONESHOT_MAX``, halved at
         8 ranks; the buffer cap) with what this node's xGMI topology measures.  ``route=False``
-        keeps the kernels' range (gloo groups chunk large messages through them)."""
+        keeps the kernels' range (gloo groups chunk large messages through them).  With `hidden`
+        the fused all-reduce + add + RMSNorm kernels are timed too, on [nb / 2 / hidden, hidden]
+        rows, and their own one-shot limit routes ``all_reduce_add_rmsnorm``.
+
+        Messages up to ``DECODE_FLOOR`` always stay on the kernels whatever RCCL measures: the
+        decode graphs capture these calls, and an RCCL call inside a captured step is a path this
+        build does not test."""
         import torch.distributed as dist
         sizes = sizes or [nb for nb in (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20) if nb <= self.cap_bytes]
         dev = torch.device("cuda", torch.cuda.current_device())
-        table = torch.zeros(3, len(sizes), dtype=torch.float64, device=dev)
+        table = torch.zeros(5, len(sizes), dtype=torch.float64, device=dev)
         for i, nb in enumerate(sizes):
             x = torch.zeros(nb // 2, dtype=torch.bfloat16, device=dev)
-            fns = (lambda: self.all_reduce_(x, mode=1), lambda: self.all_reduce_(x, mode=2),
-                   lambda: dist.all_reduce(x, group=group))
+            fns = [lambda: self.all_reduce_(x, mode=1), lambda: self.all_reduce_(x, mode=2),
+                   lambda: dist.all_reduce(x, group=group)]
+            if hidden:
+                rows = max(1, nb // (2 * hidden))
+                xa = torch.zeros(rows, hidden, dtype=torch.bfloat16, device=dev)
+                ra, wa = torch.zeros_like(xa), torch.ones(hidden, dtype=torch.bfloat16, device=dev)
+                fns += [lambda: self.all_reduce_add_rmsnorm(xa, ra, wa, 1e-6, mode=1),
+                        lambda: self.all_reduce_add_rmsnorm(xa, ra, wa, 1e-6, mode=2)]
             for m, fn in enumerate(fns):
                 fn()
                 torch.cuda.synchronize()
@@ -171,11 +187,17 @@ class _Rank:
         dist.all_reduce(table, op=dist.ReduceOp.MAX, group=group)
         t = table.cpu().tolist()
         self.oneshot_limit, route_max = pick_thresholds(sizes, t[0], t[1], t[2], self.cap_bytes)
+        route_max = max(route_max, min(self.cap_bytes, DECODE_FLOOR))
         if route:
             self.route_max = route_max
+        if hidden:
+            self.addnorm_oneshot_limit = pick_thresholds(sizes, t[3], t[4], t[2], self.cap_bytes)[0]
         self.calls = {1: 0, 2: 0}
         self.calibration = {"sizes": sizes, "oneshot_us": t[0], "twoshot_us": t[1], "rccl_us": t[2],
                             "oneshot_limit": self.oneshot_limit, "route_max": route_max}
+        if hidden:
+            self.calibration.update(addnorm_oneshot_us=t[3], addnorm_twoshot_us=t[4],
+                                    addnorm_oneshot_limit=self.addnorm_oneshot_limit, hidden=hidden)
         return self.calibration
 
     def error_async(self, host: torch.Tensor, stream) -> None:
@@ -193,25 +215,34 @@ class _Rank:
         return (self.can(x) and x.dim() == 2 and x.shape[1] % 8 == 0 and x.shape[1] <= THREADS * 16)
 
     def all_reduce_add_rmsnorm(self, x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
-                               stream=None) -> torch.Tensor:
-        """residual <- residual + sum_ranks(x); returns rmsnorm(residual) * w (one kernel, one-shot)."""
+                               stream=None, mode: Optional[int] = None) -> torch.Tensor:
+        """residual <- residual + sum_ranks(x); returns rmsnorm(residual) * w -- one kernel, one-shot
+        up to the fused kernels' own measured limit (``calibrate(hidden=...)``), two-shot above
+        (rows split over the ranks; identical bits)."""
         if not self.can_addnorm(x):
             raise ValueError("fused all-reduce + RMSNorm: contiguous bf16 [rows, H<=8192], within the cap")
         rows, H = x.shape
         if not (residual.shape == x.shape and residual.is_contiguous() and residual.dtype == torch.bfloat16
                 and w.shape == (H,) and w.dtype == torch.bfloat16):
             raise ValueError("fused all-reduce + RMSNorm: residual [rows, H] bf16, weight [H] bf16")
+        nbytes = 2 * x.numel()
+        if mode is None:
+            limit = self.addnorm_oneshot_limit
+            mode = (choose_mode(nbytes, self.world, self.oneshot_max) if limit is None
+                    else 1 if nbytes <= limit else 2)
         h = torch.empty_like(x)
-        blocks = int(min(self.max_blocks, rows))
+        per = rows if mode == 1 else -(-rows // self.world)
+        blocks = int(max(1, min(self.max_blocks, per)))
         s = (stream or torch.cuda.current_stream()).cuda_stream
         rc = self.lib.bcg_ar_allreduce_addnorm(self._data, self._sig, self.rank, self.world,
                                                ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(residual.data_ptr()),
                                                ctypes.c_void_p(w.data_ptr()), ctypes.c_void_p(h.data_ptr()), rows,
-                                               H, float(eps), self.cap_bytes, blocks, self.timeout_s,
+                                               H, float(eps), self.cap_bytes, blocks, self.timeout_s, mode,
                                                ctypes.c_void_p(s))
         if rc != 0:
             raise RuntimeError(f"bcg_ar_allreduce_addnorm launch failed (rc={rc})")
-        self.calls[3] = self.calls.get(3, 0) + 1
+        key = 3 if mode == 1 else 4
+        self.calls[key] = self.calls.get(key, 0) + 1
         return h
 
     def take_error(self) -> bool:

@@ -87,12 +87,14 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) ->
     return lay
 
 
-def tensor_parallel_group(tp: int, custom_allreduce: bool = False) -> TPGroup:
+def tensor_parallel_group(tp: int, custom_allreduce: bool = False, hidden: Optional[int] = None) -> TPGroup:
     """TPGroup of this rank (every rank must call this with the same arguments).
 
     ``custom_allreduce``: also map the TP peers' buffers for the xGMI one-/two-shot
     all-reduce kernels (RCCL process groups on GPUs only; set
-    ``BCG_CUSTOM_AR=0`` to force RCCL for every collective).
+    ``BCG_CUSTOM_AR=0`` to force RCCL for every collective).  ``hidden``: the model's
+    hidden size -- the calibration also times the fused all-reduce + add + RMSNorm
+    kernels on rows of that width and routes them by their own one-shot limit.
     """
     if tp <= 1:
         return TPGroup()
@@ -126,7 +128,8 @@ def tensor_parallel_group(tp: int, custom_allreduce: bool = False) -> TPGroup:
             # built-in rule, =force also calibrates over gloo -- one-GPU tests of the mechanism)
             cal = os.environ.get("BCG_AR_CALIBRATE", "1")
             if cal == "force" or (cal != "0" and dist.get_backend(_TP_GROUPS[tp]) == "nccl"):
-                _CUSTOM_AR[tp].calibrate(_TP_GROUPS[tp], route=dist.get_backend(_TP_GROUPS[tp]) == "nccl")
+                _CUSTOM_AR[tp].calibrate(_TP_GROUPS[tp], route=dist.get_backend(_TP_GROUPS[tp]) == "nccl",
+                                         hidden=hidden)
         custom = _CUSTOM_AR[tp]
     return TPGroup(_TP_GROUPS[tp], lay.tp_rank, tp, custom=custom, ctrl=_TP_CTRL[tp],
                    leader=lay.rank - lay.tp_rank, chunk_large=dist.get_backend(_TP_GROUPS[tp]) == "gloo")

@@ -12,8 +12,9 @@
 //   two-shot  : reduce-scatter (rank r reduces slice r from every peer) +
 //               all-gather (read the other reduced slices from their owners):
 //               2(n-1)/n of the message per rank, spread over all n-1 links;
-//   addnorm   : one-shot fused with the residual update + RMSNorm that follows
-//               the row-parallel o/down projections (one kernel, rows per block).
+//   addnorm   : the all-reduce fused with the residual update + RMSNorm that follows
+//               the row-parallel o/down projections (one kernel, rows per block), in a
+//               one-shot and a two-shot (rows split over the ranks) form.
 //
 // Hand-off protocol (MI355X_MICROARCH.md "inter-workgroup visibility", at
 // system instead of agent scope because the consumer is another GPU):
@@ -251,6 +252,109 @@ __global__ __launch_bounds__(AR_THREADS) void ar_oneshot_addnorm_kernel(
   ar_end(me);
 }
 
+// Two-shot form of the fused all-reduce + add + RMSNorm (prefill-sized messages): rank r owns
+// rows [r S, (r+1) S), S = ceil(rows / W).
+//   1. every rank stages its whole partial (block b: rows s S + b + k nblk of every slice s);
+//   2. reduce-scatter: the owner sums its rows over every rank (fixed rank order), updates the
+//      residual, writes the new residual rows to its result region and normalises them;
+//   3. all-gather: every other row's new residual comes from its owner's result region and is
+//      normalised locally -- the same bf16 inputs and the same arithmetic as the owner's, so h is
+//      bitwise identical on every rank and to the one-shot kernel.
+// Link bytes per rank 2 (W-1)/W of the message (one-shot: W-1), spread over all W-1 links.
+template <int W>
+__device__ __forceinline__ void ar_norm_row(const float (&v)[AR_ROW_VECS][8], float ss, const u16x8* __restrict__ w,
+                                            u16x8* __restrict__ h_row, int hv, float eps, float* s_part) {
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int k = 0; k < AR_THREADS / WAVE; ++k) tot += s_part[k];
+  const float inv = rsqrtf(tot / (hv * 8) + eps);
+#pragma unroll
+  for (int c = 0; c < AR_ROW_VECS; ++c) {
+    const int i = threadIdx.x + c * AR_THREADS;
+    if (i < hv) {
+      const u16x8 wv = w[i];
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[c][j] * inv * bf2f(wv[j]));
+      h_row[i] = o;
+    }
+  }
+  __syncthreads();  // s_part reused by the next row
+}
+
+template <int W>
+__global__ __launch_bounds__(AR_THREADS) void ar_twoshot_addnorm_kernel(
+    ArPeers P, int rank, const u16x8* __restrict__ in, u16x8* residual, const u16x8* __restrict__ w,
+    u16x8* __restrict__ h_out, int rows, int hv /* H / 8 */, float eps, int64_t cap_vec, uint64_t timeout_ticks) {
+  __shared__ float s_part[AR_THREADS / WAVE];
+  ArSignal* me = P.sig[rank];
+  const uint32_t epoch = ar_begin(me);
+  const int64_t off = static_cast<int64_t>(epoch & 1u) * 2 * cap_vec;
+  u16x8* mine = P.data[rank] + off;
+  const int S = (rows + W - 1) / W;
+  // 1. stage this block's rows of every slice
+  for (int s = 0; s < W; ++s)
+    for (int r = s * S + blockIdx.x; r < min((s + 1) * S, rows); r += gridDim.x)
+      for (int i = threadIdx.x; i < hv; i += AR_THREADS)
+        mine[static_cast<int64_t>(r) * hv + i] = in[static_cast<int64_t>(r) * hv + i];
+  ar_signal(P, rank, W, 0, epoch);
+  ar_wait(P, rank, W, 0, epoch, timeout_ticks);
+  // 2. reduce-scatter + residual update + norm of the owned rows
+  for (int r = rank * S + blockIdx.x; r < min((rank + 1) * S, rows); r += gridDim.x) {
+    float v[AR_ROW_VECS][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < AR_ROW_VECS; ++c) {
+      const int i = threadIdx.x + c * AR_THREADS;
+      if (i < hv) {
+        const int64_t e = static_cast<int64_t>(r) * hv + i;
+        const u16x8 sum = ar_sum<W>(P, off, e);
+        const u16x8 res = residual[e];
+        u16x8 nr;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          nr[j] = f2bf(bf2f(res[j]) + bf2f(sum[j]));
+          v[c][j] = bf2f(nr[j]);
+          ss += v[c][j] * v[c][j];
+        }
+        residual[e] = nr;
+        mine[cap_vec + e] = nr;
+      }
+    }
+    ar_norm_row<W>(v, ss, w, h_out + static_cast<int64_t>(r) * hv, hv, eps, s_part);
+  }
+  ar_signal(P, rank, W, 1, epoch);
+  ar_wait(P, rank, W, 1, epoch, timeout_ticks);
+  // 3. all-gather the other slices' new residual rows, normalise them here
+  for (int s = 0; s < W; ++s) {
+    if (s == rank) continue;
+    const u16x8* src = P.data[s] + off + cap_vec;
+    for (int r = s * S + blockIdx.x; r < min((s + 1) * S, rows); r += gridDim.x) {
+      float v[AR_ROW_VECS][8];
+      float ss = 0.f;
+#pragma unroll
+      for (int c = 0; c < AR_ROW_VECS; ++c) {
+        const int i = threadIdx.x + c * AR_THREADS;
+        if (i < hv) {
+          const int64_t e = static_cast<int64_t>(r) * hv + i;
+          const u16x8 nr = src[e];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            v[c][j] = bf2f(nr[j]);
+            ss += v[c][j] * v[c][j];
+          }
+          residual[e] = nr;
+        }
+      }
+      ar_norm_row<W>(v, ss, w, h_out + static_cast<int64_t>(r) * hv, hv, eps, s_part);
+    }
+  }
+  ar_end(me);
+}
+
 template <int W>
 int launch_ar(const ArPeers& P, int rank, const void* in, void* out, int64_t nvec, int64_t cap_vec, int mode,
               int blocks, uint64_t ticks, hipStream_t stream) {
@@ -336,14 +440,15 @@ BCG_API int bcg_ar_set_error(void* sig) {
   return hipMemcpy(&s->error, &one, sizeof(one), hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
 }
 
-// Fused one-shot all-reduce + residual add + RMSNorm over [rows, H] bf16 (see the kernel).
+// Fused all-reduce + residual add + RMSNorm over [rows, H] bf16 (see the kernels): mode 1 =
+// one-shot, 2 = two-shot (rows split over the ranks).  Identical bits either way.
 BCG_API int bcg_ar_allreduce_addnorm(void* const* data, void* const* sig, int rank, int world, const void* in,
                                      void* residual, const void* weight, void* h_out, int rows, int H, float eps,
-                                     int64_t cap_bytes, int blocks, double timeout_s, hipStream_t stream) {
+                                     int64_t cap_bytes, int blocks, double timeout_s, int mode, hipStream_t stream) {
   if (world < 2 || world > AR_MAX_RANKS || (world & (world - 1)) || rank < 0 || rank >= world) return -2;
   if (rows <= 0 || H % 8 || H > AR_THREADS * 8 * AR_ROW_VECS || static_cast<int64_t>(rows) * H * 2 > cap_bytes)
     return -2;
-  if (blocks < 1 || blocks > AR_MAX_BLOCKS || cap_bytes % 16) return -2;
+  if (blocks < 1 || blocks > AR_MAX_BLOCKS || cap_bytes % 16 || (mode != 1 && mode != 2)) return -2;
   ArPeers P{};
   for (int r = 0; r < world; ++r) {
     if (!data[r] || !sig[r]) return -2;
@@ -360,19 +465,19 @@ BCG_API int bcg_ar_allreduce_addnorm(void* const* data, void* const* sig, int ra
   const u16x8* wv = static_cast<const u16x8*>(weight);
   u16x8* ho = static_cast<u16x8*>(h_out);
   const int hv = H / 8;
+#define BCG_AR_ADDNORM(WW)                                                                                        \
+  if (mode == 1)                                                                                                  \
+    hipLaunchKernelGGL(ar_oneshot_addnorm_kernel<WW>, dim3(blocks), dim3(AR_THREADS), 0, stream, P, rank, src, res, \
+                       wv, ho, rows, hv, eps, cap_vec, ticks);                                                   \
+  else                                                                                                            \
+    hipLaunchKernelGGL(ar_twoshot_addnorm_kernel<WW>, dim3(blocks), dim3(AR_THREADS), 0, stream, P, rank, src, res, \
+                       wv, ho, rows, hv, eps, cap_vec, ticks);
   switch (world) {
-    case 2:
-      hipLaunchKernelGGL(ar_oneshot_addnorm_kernel<2>, dim3(blocks), dim3(AR_THREADS), 0, stream, P, rank, src, res,
-                         wv, ho, rows, hv, eps, cap_vec, ticks);
-      break;
-    case 4:
-      hipLaunchKernelGGL(ar_oneshot_addnorm_kernel<4>, dim3(blocks), dim3(AR_THREADS), 0, stream, P, rank, src, res,
-                         wv, ho, rows, hv, eps, cap_vec, ticks);
-      break;
-    default:
-      hipLaunchKernelGGL(ar_oneshot_addnorm_kernel<8>, dim3(blocks), dim3(AR_THREADS), 0, stream, P, rank, src, res,
-                         wv, ho, rows, hv, eps, cap_vec, ticks);
+    case 2: BCG_AR_ADDNORM(2) break;
+    case 4: BCG_AR_ADDNORM(4) break;
+    default: BCG_AR_ADDNORM(8)
   }
+#undef BCG_AR_ADDNORM
   return BCG_CHECK_LAUNCH();
 }
 

@@ -44,6 +44,10 @@ def test_pick_thresholds_from_measured_table():
     assert CA.pick_thresholds(sizes, [9] * 5, [5] * 5, [99] * 5, 32 << 20) == (0, 32 << 20)
     # only a prefix of wins counts (a win above the first loss is measurement noise)
     assert CA.pick_thresholds(sizes, [1, 9, 1, 1, 1], [5] * 5, [99] * 5, 32 << 20)[0] == 64 << 10
+    # the route follows the kernel actually picked at each size: one-shot loses to
+    # two-shot from 64 KiB on, so at 256 KiB it is two-shot (80 us) against RCCL (60 us) --
+    # one-shot's 30 us there must not keep the size on the kernels
+    assert CA.pick_thresholds(sizes[:2], [10, 30], [5, 80], [20, 60], 32 << 20) == (0, 64 << 10)
 
 
 class _FakeCustom:
@@ -94,6 +98,18 @@ def test_tp_group_chunks_large_messages_over_gloo(monkeypatch):
     assert fake.calls == 3 and seen == ["pg"]
 
 
+_STREAMS = []
+
+
+def _rank_streams(world):
+    """ONE set of rank streams for every in-process test: with GPU_MAX_HW_QUEUES=4, streams
+    created per test pile up, and two rank streams that land on one hardware queue deadlock
+    (rank 1's kernel queued behind rank 0's spinning one) until the kernels' timeout."""
+    while len(_STREAMS) < world:
+        _STREAMS.append(torch.cuda.Stream())
+    return _STREAMS[:world]
+
+
 def _ref_sum(xs):
     acc = xs[0].float().clone()
     for x in xs[1:]:
@@ -107,7 +123,7 @@ def test_local_ranks_allreduce_bitwise(world, sizes):
     """In-process: only world 2 -- with GPU_MAX_HW_QUEUES=4 a third or fourth rank stream
     can share a hardware queue with another rank's spinning kernel (4 ranks: see the IPC test)."""
     lr = CA.LocalRanks(world, cap_bytes=8 << 20, timeout_s=5.0)
-    streams = [torch.cuda.Stream() for _ in range(world)]
+    streams = _rank_streams(world)
     try:
         for it in range(3):  # successive calls exercise the epoch flags and parity buffers
             for n in sizes:
@@ -124,6 +140,44 @@ def test_local_ranks_allreduce_bitwise(world, sizes):
                     assert not lr.ranks[r].take_error(), f"rank {r}: barrier timeout (n={n})"
                     assert torch.equal(bufs[r], ref), f"rank {r} n={n} it={it}"
         assert lr.ranks[0].calls[1] > 0 and lr.ranks[0].calls[2] > 0  # 5120*300 bf16 = 3 MiB: two-shot
+    finally:
+        lr.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", [1, 8, 77, 1291])
+def test_local_ranks_addnorm_oneshot_twoshot_identical(rows):
+    """Fused all-reduce + residual add + RMSNorm, world 2 in one process: the two-shot form
+    (rows split over the ranks, new residual rows gathered and normalised locally) gives the
+    same bits as the one-shot form and matches the fp32 reference of the unfused ops."""
+    H, world = 5120, 2
+    lr = CA.LocalRanks(world, cap_bytes=16 << 20, timeout_s=5.0)
+    streams = _rank_streams(world)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(rows)
+        xs = [(torch.randn(rows, H, device="cuda", generator=g) * 0.1).to(torch.bfloat16) for _ in range(world)]
+        res0 = torch.randn(rows, H, device="cuda", generator=g).to(torch.bfloat16)
+        w = (torch.rand(H, device="cuda", generator=g) + 0.5).to(torch.bfloat16)
+        outs = {}
+        for mode in (1, 2, 2, 1):  # alternate: epochs / parity buffers advance between forms
+            res = [res0.clone() for _ in range(world)]
+            hs = [None] * world
+            torch.cuda.synchronize()
+            for r in range(world):
+                with torch.cuda.stream(streams[r]):
+                    hs[r] = lr.ranks[r].all_reduce_add_rmsnorm(xs[r], res[r], w, 1e-6, mode=mode)
+            torch.cuda.synchronize()
+            for r in range(world):
+                assert not lr.ranks[r].take_error()
+            assert torch.equal(hs[0], hs[1]) and torch.equal(res[0], res[1])
+            outs.setdefault(mode, (hs[0], res[0]))
+            assert torch.equal(hs[0], outs[mode][0])
+        assert torch.equal(outs[1][0], outs[2][0]) and torch.equal(outs[1][1], outs[2][1])
+        nr = (res0.float() + _ref_sum(xs).float()).to(torch.bfloat16)
+        ref_h = nr.float() * torch.rsqrt(nr.float().pow(2).mean(-1, keepdim=True) + 1e-6) * w.float()
+        assert torch.equal(outs[2][1], nr)
+        assert (outs[2][0].float() - ref_h).abs().max().item() / ref_h.abs().max().item() < 1e-2
+        assert lr.ranks[0].calls.get(3, 0) == 2 and lr.ranks[0].calls.get(4, 0) == 2
     finally:
         lr.close()
 
@@ -244,5 +298,8 @@ def test_ipc_tp_collectives_real_shapes(tmp_path, world, back_to_back, cap_mb):
     for r in range(world):
         res = json.load(open(f"{out}.{r}"))
         print(f"[tp-collectives] world={world} back_to_back={back_to_back} cap={cap_mb}MB rank={r} {res}")
-        assert not res["err"] and res["calls"].get("3", 0) == (6 if cap_mb >= 16 else 2 + 4 * 4), (r, res)
+        fused = res["calls"].get("3", 0) + res["calls"].get("4", 0)  # one-shot + two-shot fused calls
+        assert not res["err"] and fused == (6 if cap_mb >= 16 else 2 + 4 * 4), (r, res)
+        if cap_mb >= 16:  # the 13 MB prefill message takes the two-shot form, decode the one-shot
+            assert res["calls"].get("4", 0) == 4 and res["calls"].get("3", 0) == 2, (r, res)
         assert max(res["errs"]) < 2e-2, (r, res)
