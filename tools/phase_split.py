@@ -23,7 +23,8 @@ csv.field_size_limit(sys.maxsize)
 FAMILIES = [  # (substring of the kernel name, family); first match wins
     ("decode_shared_kernel", "attn_decode_shared"), ("decode_attn_kernel", "attn_decode"),
     ("decode_combine_kernel", "attn_decode_combine"), ("prefill_attn", "attn_prefill"),
-    ("gemm_pp_kernel", "gemm_hand_256x256"), ("gemm_nt_kernel", "gemm_hand_tiles"), ("Cijk_", "gemm_hipblaslt"),
+    ("gemm_w4_kernel", "gemm_hand_w4"), ("gemm_pp_kernel", "gemm_hand_256x256"), ("gemm_nt_kernel", "gemm_hand_tiles"),
+    ("Cijk_", "gemm_hipblaslt"),
     ("qk_norm_rope", "rope_kv"), ("rmsnorm", "norm"), ("silu_mul", "silu_mul"), ("sample", "sampler"),
 ]
 
