@@ -306,6 +306,8 @@ def main(argv=None):
     import torch.distributed as dist
 
     gpu = args.backend == "hip"
+    if args.backend == "hostmodel":
+        os.environ.setdefault("BCG_HOSTMODEL_TOKENS_S", "34000")
     ctrl = None
     if args.one_device:
         local = 0
@@ -335,6 +337,8 @@ def main(argv=None):
                            use_hip_graphs=not args.no_graphs, prefix_caching=not args.no_prefix_cache,
                            overlap_prefill=args.overlap_prefill, custom_allreduce=not args.no_custom_allreduce,
                            kv_cache_dtype=args.kv_cache_dtype)
+    if C.ENGINE_CONFIG.get("num_layers_override"):
+        raise SystemExit("bench.py: num_layers_override (reduced depth) is a test option, never a measurement")
     if args.max_batch_seqs:
         C.ENGINE_CONFIG["max_batch_seqs"] = args.max_batch_seqs
     if args.kv_cache_gb:
@@ -409,6 +413,7 @@ def main(argv=None):
     if gpu:
         torch.cuda.synchronize()
     t_start = time.perf_counter()
+    cpu0 = time.process_time()  # this rank's host CPU (all threads) over the timed region
     a0 = accepted()
     per_window, steps_done, last = [], 0, a0
     # the deadline is agreed on by every rank (the slowest start wins)
@@ -425,6 +430,7 @@ def main(argv=None):
         last = now
         steps_done += 1
     decisions = last - a0
+    host_cpu_s = time.process_time() - cpu0
     if gpu:
         torch.cuda.synchronize()
     barrier()
@@ -455,6 +461,16 @@ def main(argv=None):
         dist.all_reduce(tt, op=dist.ReduceOp.SUM, group=ctrl)
         tok = float(tt[0])
     tokens_per_s = tok / elapsed if elapsed > 0 else 0.0
+    # host budget: CPU seconds of every rank's process over the timed region (summed) and the
+    # slowest DP replica's decision rate
+    per_rank_rate = decisions / elapsed if elapsed > 0 and pool is not None else float("inf")
+    if world > 1:
+        hc = torch.tensor([host_cpu_s], dtype=torch.float64)
+        dist.all_reduce(hc, op=dist.ReduceOp.SUM, group=ctrl)
+        host_cpu_s = float(hc[0])
+        mr = torch.tensor([per_rank_rate], dtype=torch.float64)
+        dist.all_reduce(mr, op=dist.ReduceOp.MIN, group=ctrl)
+        per_rank_rate = float(mr[0])
     stats = window_stats(per_window, args.window_s)
     if rank == 0:
         line = {
@@ -487,6 +503,11 @@ def main(argv=None):
                        "fill_s": round(fill_s, 1), "fill_max_s": args.fill_max_s,
                        "fill_capped": fill_s >= args.fill_max_s - 0.5,
                        "tokens_per_s": round(tokens_per_s, 1), "window_stats_rank0": stats,
+                       "host": {"cpu_s_all_ranks": round(host_cpu_s, 1),
+                                "cpu_s_per_decision": (round(host_cpu_s / total_decisions, 4)
+                                                       if total_decisions else None),
+                                "min_replica_decisions_per_s": round(per_rank_rate, 3),
+                                "host_cpus": os.cpu_count()},
                        "age_mix": {"p": args.age_p, "burnin_chars": args.burnin_chars,
                                    "mean_burnin_rounds": (round(sum(pool.ages) / len(pool.ages), 2)
                                                           if pool else None),

@@ -103,4 +103,6 @@ ENGINE_CONFIG = {
     # hipBLASLt's stream-K prefill GEMMs (inter-workgroup waits) beside a second
     # persistent kernel can starve each other -- one run hung.
     "overlap_prefill": os.environ.get("BCG_OVERLAP_PREFILL", "0") == "1",
+    # tests only: run the model with this many decoder layers (real layer shapes, reduced depth)
+    "num_layers_override": None,
 }

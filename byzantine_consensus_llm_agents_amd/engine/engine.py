@@ -107,6 +107,11 @@ class EngineArgs:
         weights = weights or ec.get("weights") or "auto"
         model_dir = weights if weights not in ("auto", "random") else None
         cfg = get_model_config(model, model_dir)
+        if ec.get("num_layers_override"):
+            # reduced depth at the real layer shapes: end-to-end tests of large configurations
+            # (TP engines on a one-GPU box) -- never a measurement (bench.py refuses it)
+            import dataclasses
+            cfg = dataclasses.replace(cfg, num_layers=int(ec["num_layers_override"]))
         args = cls(model=model, model_cfg=cfg, backend=backend,
                    weights="random" if weights == "auto" else weights, seed=seed,
                    kv_block_size=ec.get("kv_block_size", 16),

@@ -230,3 +230,64 @@ class BurnInLLM:
             schema = sp.guided_decoding.json if sp is not None and sp.guided_decoding is not None else None
             outs.append(RequestOutput(i, p, [CompletionOutput(0, self._answer(p, schema))]))
         return outs
+
+
+class HostModelBackend:
+    """Engine stand-in that does the real engine's HOST work and models its GPU time.
+
+    For measuring whether the host keeps up with several DP ranks per node:
+    every call tokenizes its prompts with the model's tokenizer, produces schema-valid outputs
+    of the measured mean lengths (:class:`BurnInLLM`; votes drawn by :func:`scripted_object`, so
+    games do end), re-tokenizes and detokenizes them (the engine's sampler produces ids, the
+    detokenizer text), and waits for a modelled GPU: one FIFO device that processes
+    ``tokens_per_s`` (uncached prompt + generated) tokens per second -- the measured rate of the
+    real engine -- with ``cached_frac`` of the prompt tokens served by the prefix cache.  The
+    real engine batches calls on the device; the model keeps only its throughput, which is what
+    the host has to sustain.
+    """
+
+    name = "hostmodel"
+    async_mode = True  # calls run concurrently (as under continuous batching)
+
+    def __init__(self, model: str, seed: int = 0, tokens_per_s: float = 34000.0, cached_frac: float = 0.375,
+                 strategy_chars: int = 310, reasoning_chars: int = 410):
+        import threading
+
+        from .tokenizer import load_tokenizer
+        self.tok = load_tokenizer(model)
+        self.rate, self.cached_frac, self.seed = tokens_per_s, cached_frac, seed
+        self.burn = BurnInLLM(strategy_chars, reasoning_chars, seed)
+        self.lock = threading.Lock()
+        self.free_at = 0.0
+        self.stats = {"prompt_tokens": 0, "cached_tokens": 0, "generated_tokens": 0, "calls": 0}
+
+    def _answer(self, prompt: str, schema: Optional[Dict]) -> str:
+        if schema and "decision" in schema.get("properties", {}):
+            return json.dumps(scripted_object(prompt, schema, self.seed))
+        return self.burn._answer(prompt, schema)
+
+    def generate(self, prompts, params_list):
+        import time
+        t0 = time.perf_counter()
+        schemas = [p.guided_decoding.json if p.guided_decoding is not None else None for p in params_list]
+        p_ids = self.tok.encode_batch(list(prompts))
+        out_ids = self.tok.encode_batch([self._answer(p, s) for p, s in zip(prompts, schemas)])
+        texts = [self.tok.decode(ids) for ids in out_ids]
+        n_prompt = sum(len(i) for i in p_ids)
+        n_cached = int(self.cached_frac * n_prompt)
+        n_gen = sum(len(i) for i in out_ids)
+        with self.lock:
+            start = max(t0, self.free_at)
+            self.free_at = start + (n_prompt - n_cached + n_gen) / self.rate
+            done = self.free_at
+            self.stats["prompt_tokens"] += n_prompt
+            self.stats["cached_tokens"] += n_cached
+            self.stats["generated_tokens"] += n_gen
+            self.stats["calls"] += 1
+        delay = done - time.perf_counter()
+        if delay > 0:
+            time.sleep(delay)
+        return texts
+
+    def shutdown(self):
+        pass

@@ -9,7 +9,9 @@ Backends:
   * ``hip``   - :class:`..engine.engine.InferenceEngine` with the HIP kernels
                 (MI355X); fails loudly if the kernel library is missing;
   * ``torch`` - the same engine on PyTorch reference ops (CPU tests);
-  * ``fake``  - scripted schema-valid answers (plumbing, parity tests).
+  * ``fake``  - scripted schema-valid answers (plumbing, parity tests);
+  * ``hostmodel`` - the engine's host work (tokenize, detokenize) with a modelled GPU at a
+                measured token rate (host-budget measurements of several DP ranks).
 
 Tensor parallelism: ``tensor_parallel_size > 1`` in a process that was not
 started by a launcher spawns the TP worker processes itself (ranks 1..N-1, each
@@ -155,6 +157,12 @@ class LLM:
             from .fake import FakeBackend
             self.backend = FakeBackend(seed=seed or 0)
             # scripted engine: no model to shard; under a TP layout only each group's rank 0 serves
+            self.backend.is_driver = int(os.environ.get("RANK", "0")) % max(1, tensor_parallel_size) == 0
+        elif self.backend_name == "hostmodel":
+            # host work of the real engine + a modelled GPU (host-budget measurements, bench.py)
+            from .fake import HostModelBackend
+            self.backend = HostModelBackend(model, seed=seed or 0,
+                                            tokens_per_s=float(os.environ.get("BCG_HOSTMODEL_TOKENS_S", "34000")))
             self.backend.is_driver = int(os.environ.get("RANK", "0")) % max(1, tensor_parallel_size) == 0
         elif self.backend_name in ("hip", "torch"):
             if tensor_parallel_size > 1:

@@ -94,3 +94,18 @@ def test_window_stats_block_estimate():
     s = window_stats([100, 300] * 4, 12.0)  # perfectly anti-correlated neighbours
     assert s["se_pct"] > 10 and s["block4_se_pct"] == 0.0
     assert window_stats([5], 12.0) == {"n": 1}
+
+
+def test_bench_hostmodel_backend_reports_host_budget():
+    """--backend hostmodel: the engine's host work with a modelled GPU; detail.host carries the
+    CPU seconds per decision and the slowest replica's rate."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--backend", "hostmodel", "--sims-per-gpu", "4",
+           "--honest", "4", "--byzantine", "1", "--window-s", "2", "--steps", "2", "--warmup", "1"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", BCG_HOSTMODEL_TOKENS_S="200000")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    h = out["detail"]["host"]
+    assert out["detail"]["decisions"] > 0 and h["cpu_s_per_decision"] > 0
+    assert h["min_replica_decisions_per_s"] > 0 and out["detail"]["tokens_per_s"] > 0
