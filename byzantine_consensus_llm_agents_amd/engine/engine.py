@@ -287,7 +287,13 @@ class InferenceEngine:
         a, m = self.args, self.model
         rows = min(MAX_ROWS, max(a.max_batch_seqs, 1))
         max_blocks = (a.max_model_len + a.kv_block_size - 1) // a.kv_block_size
-        return 4 * self.ops.decode_workspace_numel(rows, m.n_q, m.hd, max_blocks, a.kv_block_size)
+        cascade = bool(a.cascade_decode)
+        limit = self.ops.decode_max_context(cascade)
+        if max_blocks * a.kv_block_size > limit:  # fail at init, not with rc -3 at the first decode
+            raise ValueError(f"max_model_len {a.max_model_len} exceeds the decode attention limit of {limit} "
+                             f"tokens ({'with' if cascade else 'without'} shared-prefix decode; "
+                             "cascade_decode=False allows 16384)")
+        return 4 * self.ops.decode_workspace_numel(rows, m.n_q, m.hd, max_blocks, a.kv_block_size, cascade)
 
     def _load_tuned_gemms(self):
         """Load PyTorch TunableOp results for this model's decode GEMM shapes (lookups only).

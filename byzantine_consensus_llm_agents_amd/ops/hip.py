@@ -44,7 +44,8 @@ def load_library(path: str = None) -> ctypes.CDLL:
                                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                                         c_void_p, c_int, c_int, c_void_p],
         "bcg_decode_split_tokens": [c_int, c_int, c_int],
-        "bcg_decode_max_splits": [c_int],
+        "bcg_decode_max_splits": [c_int, c_int],
+        "bcg_decode_max_context": [c_int],
         "bcg_quant_fp8": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
         "bcg_add_rmsnorm_fp8": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_int,
                                 c_void_p],
@@ -155,10 +156,10 @@ def hip_ops() -> SimpleNamespace:
             n_q, n_kv, head_dim, NB, BS, eps, _kv_fp8(k_cache, v_cache), _stream()), "qk_norm_rope_kv_write")
         return q
 
-    def decode_workspace_numel(B, n_q, hd, max_blocks, block_size=16):
-        """fp32 split partials (o, m, l) of the flash-decoding split-K (+ slot 0 of the
-        shared-prefix pass)."""
-        max_splits = lib.bcg_decode_max_splits(max_blocks * block_size)
+    def decode_workspace_numel(B, n_q, hd, max_blocks, block_size=16, cascade=True):
+        """fp32 split partials (o, m, l) of the flash-decoding split-K (+ the shared-prefix
+        pass's slots when `cascade`)."""
+        max_splits = lib.bcg_decode_max_splits(max_blocks * block_size, int(cascade))
         return B * n_q * max_splits * (hd + 2)
 
     def paged_attention_decode(q, k_cache, v_cache, layer, block_tables, seq_lens, scale, workspace=None,
@@ -174,7 +175,7 @@ def hip_ops() -> SimpleNamespace:
         max_blocks = block_tables.shape[1]
         _req(B <= 2048, "decode attention: at most 2048 rows")
         split = lib.bcg_decode_split_tokens(B, n_kv, max_blocks * BS)
-        max_splits = lib.bcg_decode_max_splits(max_blocks * BS)
+        max_splits = lib.bcg_decode_max_splits(max_blocks * BS, int(cascade is not None))
         need = B * n_q * max_splits * (hd + 2)
         if workspace is None:
             ws = torch.empty(need, dtype=torch.float32, device=q.device)
@@ -489,6 +490,7 @@ def hip_ops() -> SimpleNamespace:
                            qk_norm_rope_kv_write=qk_norm_rope_kv_write,
                            paged_attention_decode=paged_attention_decode,
                            decode_workspace_numel=decode_workspace_numel,
+                           decode_max_context=lambda cascade=True: lib.bcg_decode_max_context(int(cascade)),
                            paged_attention_prefill=paged_attention_prefill,
                            sample_step=sample_step, dispatch_log=dispatch_log,
                            library=lib)

@@ -1046,10 +1046,16 @@ constexpr int DEC_CPW = 2;
 BCG_API int bcg_decode_split_tokens(int B, int n_kv, int max_tokens) { return DEC_WAVES * CHUNK * DEC_CPW; }
 // Partial slots per (row, head): a row's own splits + up to DEC_MAX_SHARED_SPLITS of the
 // shared-prefix pass (engine/cascade.py keeps shared tokens / its split within it).
+// Only calls with the cascade tables reserve the shared slots (cascade = 0: a plain decode keeps
+// the combine kernel's 64-split limit for its own splits, i.e. 16384 tokens of context).
 constexpr int DEC_MAX_SHARED_SPLITS = 16;
-BCG_API int bcg_decode_max_splits(int max_tokens) {
+BCG_API int bcg_decode_max_splits(int max_tokens, int cascade) {
   const int split = DEC_WAVES * CHUNK * DEC_CPW;
-  return (max_tokens + split - 1) / split + DEC_MAX_SHARED_SPLITS;
+  return (max_tokens + split - 1) / split + (cascade ? DEC_MAX_SHARED_SPLITS : 0);
+}
+// Longest context a decode call supports (the combine kernel reads at most 64 splits per row).
+BCG_API int bcg_decode_max_context(int cascade) {
+  return (64 - (cascade ? DEC_MAX_SHARED_SPLITS : 0)) * DEC_WAVES * CHUNK * DEC_CPW;
 }
 
 // kv_fp8: the caches hold OCP e4m3fn bytes (scale 1) instead of bf16.

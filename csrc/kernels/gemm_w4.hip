@@ -90,6 +90,9 @@
 #define W4_ABL_PIECE0 0
 #endif
 #define W4_NPB (W4_RING5 ? 8 : W4_ABL_NPIECE)  // pieces issued in phase B
+#ifndef W4_STAGGER
+#define W4_STAGGER 0  // 1: odd waves run the loop with their pieces half a stride later
+#endif
 #ifndef W4_M0_EARLY
 #define W4_M0_EARLY 0  // 1: each piece's M0 write one MFMA ahead of the piece (needs W4_DB0 >= 1)
 #endif
@@ -128,6 +131,18 @@ __device__ __forceinline__ i32x4 make_srd(const void* base, uint32_t bytes) {
   return r;
 }
 
+// Staggered schedules (W4_STAGGER): the odd waves issue their pieces half a stride later than
+// the even waves, so the CU's four waves do not send their LDS-DMA in lock step (the same
+// device as the two loop bodies, selected by a SIMD-id bit, of hipBLASLt's MT256x256 kernel).
+struct SchedMain {
+  static constexpr int RA0 = W4_RA0, RAS = W4_RAS, DA0 = W4_DA0, DAS = W4_DAS, DB0 = W4_DB0, DBS = W4_DBS,
+                       RB0 = W4_RB0, RBS = W4_RBS;
+};
+struct SchedAlt {
+  static constexpr int RA0 = W4_RA0, RAS = W4_RAS, DA0 = W4_DA0 + W4_DAS / 2, DAS = W4_DAS,
+                       DB0 = W4_DB0 + W4_DBS / 2, DBS = W4_DBS, RB0 = W4_RB0, RBS = W4_RBS;
+  static_assert(DA0 + 7 * DAS < W4_SLOTS && DB0 + (W4_NPB - 1) * DBS < W4_SLOTS, "staggered schedule");
+};
 #ifdef W4_STAMPS
 __device__ uint64_t w4_stamps[1 << 16];  // [workgroup][wave][phase A, wait, phase B, K-tiles]
 #endif
@@ -292,7 +307,8 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   // phase B of tile t.  Past the last tile the pieces go through a zero-range descriptor: no
   // memory traffic, the zeros land in a stage nobody reads -- branch-free, one body (a
   // branch around the pieces, or two copies of the phase, made hipcc spill the accumulators)
-  auto phase_b = [&](int t, int cur) {
+  auto phase_b = [&](int t, int cur, auto sch) {
+    using Sch = decltype(sch);
     const bool more = t + 2 < nk;
     i32x4 sX, sW;
 #pragma unroll
@@ -304,18 +320,20 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       mf(idx, x1, w1);
 #ifndef W4_ABL_NODMA
 #if W4_M0_EARLY  // M0 written one MFMA before its piece (W4_DB0 >= 1)
-      if (idx + 1 >= W4_DB0 && (idx + 1 - W4_DB0) % W4_DBS == 0 && (idx + 1 - W4_DB0) / W4_DBS < W4_NPB)
-        set_m0(t + 2, (idx + 1 - W4_DB0) / W4_DBS + W4_ABL_PIECE0 + (W4_RING5 ? 8 : 0));
+      if (idx + 1 >= Sch::DB0 && (idx + 1 - Sch::DB0) % Sch::DBS == 0 && (idx + 1 - Sch::DB0) / Sch::DBS < W4_NPB)
+        set_m0(t + 2, (idx + 1 - Sch::DB0) / Sch::DBS + W4_ABL_PIECE0 + (W4_RING5 ? 8 : 0));
 #endif
-      if (idx >= W4_DB0 && (idx - W4_DB0) % W4_DBS == 0 && (idx - W4_DB0) / W4_DBS < W4_NPB)
-        dma(t + 2, (idx - W4_DB0) / W4_DBS + W4_ABL_PIECE0 + (W4_RING5 ? 8 : 0), sX, sW, W4_M0_EARLY);
+      if (idx >= Sch::DB0 && (idx - Sch::DB0) % Sch::DBS == 0 && (idx - Sch::DB0) / Sch::DBS < W4_NPB)
+        dma(t + 2, (idx - Sch::DB0) / Sch::DBS + W4_ABL_PIECE0 + (W4_RING5 ? 8 : 0), sX, sW, W4_M0_EARLY);
 #endif
 #ifndef W4_ABL_NOREAD
-      if (idx >= W4_RB0 && (idx - W4_RB0) % W4_RBS == 0 && (idx - W4_RB0) / W4_RBS < 16)
-        read_frag(t + 1, 0, (idx - W4_RB0) / W4_RBS, x0, w0);  // tile t+1 (garbage after the last)
+      if (idx >= Sch::RB0 && (idx - Sch::RB0) % Sch::RBS == 0 && (idx - Sch::RB0) / Sch::RBS < 16)
+        read_frag(t + 1, 0, (idx - Sch::RB0) / Sch::RBS, x0, w0);  // tile t+1 (garbage after the last)
 #endif
     }
   };
+  auto run = [&](auto sch) {
+    using Sch = decltype(sch);
 #ifdef W4_STAMPS  // diagnostic build: per-wave cycles in phase A / the wait + barrier / phase B
   uint64_t cyc_a = 0, cyc_w = 0, cyc_b = 0, t_end = __builtin_amdgcn_s_memtime();
 #endif
@@ -331,15 +349,15 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     for (int idx = 0; idx < W4_SLOTS; ++idx) {  // phase A
       mf(idx, x0, w0);
 #if W4_RING5  // X(t+2) into the slot W(t-1) left (free since the barrier of tile t-1)
-      if (idx >= W4_DA0 && (idx - W4_DA0) % W4_DAS == 0 && (idx - W4_DA0) / W4_DAS < 8)
-        dma(t + 2, (idx - W4_DA0) / W4_DAS, aX, aX);
+      if (idx >= Sch::DA0 && (idx - Sch::DA0) % Sch::DAS == 0 && (idx - Sch::DA0) / Sch::DAS < 8)
+        dma(t + 2, (idx - Sch::DA0) / Sch::DAS, aX, aX);
 #endif
 #ifdef W4_ABL_SPREAD  // timing ablation (racy): pieces 0..7 of tile t+2 issued in phase A
       if (idx % (W4_SLOTS / 8) == 2) dma(t + 2, idx / (W4_SLOTS / 8), srdX, srdW);
 #endif
 #ifndef W4_ABL_NOREAD
-      if (idx >= W4_RA0 && (idx - W4_RA0) % W4_RAS == 0 && (idx - W4_RA0) / W4_RAS < 16)
-        read_frag(t, 1, (idx - W4_RA0) / W4_RAS, x1, w1);
+      if (idx >= Sch::RA0 && (idx - Sch::RA0) % Sch::RAS == 0 && (idx - Sch::RA0) / Sch::RAS < 16)
+        read_frag(t, 1, (idx - Sch::RA0) / Sch::RAS, x1, w1);
 #endif
     }
 #ifdef W4_STAMPS
@@ -354,7 +372,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     const uint64_t t_w = __builtin_amdgcn_s_memtime();
     cyc_a += t_a - t_end, cyc_w += t_w - t_a;
 #endif
-    phase_b(t, cur);
+    phase_b(t, cur, sch);
 #ifdef W4_STAMPS
     t_end = __builtin_amdgcn_s_memtime();
     cyc_b += t_end - t_w;
@@ -365,6 +383,15 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     uint64_t* st = w4_stamps + (static_cast<size_t>(blockIdx.x) * 4 + wave) * 4;
     st[0] = cyc_a, st[1] = cyc_w, st[2] = cyc_b, st[3] = nk;
   }
+#endif
+  };
+#if W4_STAGGER
+  if (wave & 1)
+    run(SchedAlt{});
+  else
+    run(SchedMain{});
+#else
+  run(SchedMain{});
 #endif
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   // the last MFMAs' results are read by VALU / stores below: cover the MFMA D -> read hazard

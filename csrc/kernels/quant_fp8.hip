@@ -82,14 +82,15 @@ __global__ __launch_bounds__(QT) void add_rmsnorm_fp8_kernel(
   const int tid = threadIdx.x;
   const int nvec = H / 8;
   const size_t base = static_cast<size_t>(blockIdx.x) * H;
-  if (gather) x += static_cast<size_t>(gather[blockIdx.x]) * H - base;
+  // x row: the gathered table row (embedding lookup fused in) or this block's row
+  const bf16_t* __restrict__ xr = gather ? x + static_cast<size_t>(gather[blockIdx.x]) * H : x + base;
   float v[NORM_MAX_CHUNK][8];
   float ss = 0.f;
 #pragma unroll
   for (int c = 0; c < NORM_MAX_CHUNK; ++c) {
     const int vi = tid + c * QT;
     if (vi < nvec) {
-      const u16x8 xv = *reinterpret_cast<const u16x8*>(x + base + vi * 8);
+      const u16x8 xv = *reinterpret_cast<const u16x8*>(xr + vi * 8);
       u16x8 rv;
       if (has_residual == 1) rv = *reinterpret_cast<const u16x8*>(residual + base + vi * 8);
       u16x8 nr;
