@@ -161,6 +161,8 @@ class Fp8Plan:
             return None
         if cfg == PP_CFG:  # 256 x 256 ping-pong fp8 kernel (prefill M): N % 16, 32-bit buffer offsets
             ok = N % 16 == 0 and M * K < 1 << 32 and N * K < 1 << 32
+        elif cfg == W4_CFG:  # four-wave 256 x 256 fp8 kernel: N % 16, offsets below 2 GiB
+            ok = N % 16 == 0 and (M + 256) * K < 1 << 31 and (N + 256) * K < 1 << 31
         else:
             ok = N % self.tiles[cfg][1] == 0
         return (cfg, split) if ok else None

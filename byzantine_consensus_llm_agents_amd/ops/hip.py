@@ -239,7 +239,7 @@ def hip_ops() -> SimpleNamespace:
             return gemm_nt(x, w, cfg, 0, bias=bias)
         return torch.nn.functional.linear(x, w, bias)
 
-    from .gemm_plan import PP_CFG, GemmPlan
+    from .gemm_plan import PP_CFG, W4_CFG, GemmPlan
     plan = GemmPlan(lib)
 
     # Split-K arrival counters (one int per output tile; the last-arriving workgroup of a
@@ -429,8 +429,10 @@ def hip_ops() -> SimpleNamespace:
              and ws.numel() == N and ws.is_contiguous(), "gemm_nt_fp8: fp32 scales xs [M], ws [N]")
         bm, bn = plan.tiles[cfg]
         pp = cfg == PP_CFG  # 256 x 256 ping-pong kernel: N only a multiple of 16, 32-bit buffer offsets
-        _req(0 <= cfg <= PP_CFG and K % 128 == 0 and N % (16 if pp else bn) == 0 and 1 <= split_k <= K // 128
-             and epi in (0, 2) and (not pp or (M * K < 1 << 32 and N * K < 1 << 32)),
+        w4 = cfg == W4_CFG  # four-wave 256 x 256 kernel: N a multiple of 16, offsets below 2 GiB
+        _req(0 <= cfg <= W4_CFG and K % 128 == 0 and N % (16 if pp or w4 else bn) == 0 and 1 <= split_k <= K // 128
+             and epi in (0, 2) and (not pp or (M * K < 1 << 32 and N * K < 1 << 32))
+             and (not w4 or ((M + 256) * K < 1 << 31 and (N + 256) * K < 1 << 31)),
              f"gemm_nt_fp8: shape {M}x{N}x{K} epi {epi} split {split_k} unsupported by tile {cfg}")
         if out is None:
             out = torch.empty(M, N, dtype=torch.bfloat16, device=xq.device)

@@ -387,6 +387,9 @@ BCG_API int bcg_gemm_pp(int epi, const void* x, const void* w, const void* bias,
 constexpr int PP_CFG = N_CFG;  // the 256 x 256 ping-pong kernel (gemm_pp.hip)
 BCG_API int bcg_gemm_w4(int epi, const void* x, const void* w, const void* bias, const void* residual, void* c,
                         void* ws, void* counters, int M, int N, int K, int inter, int split_k, hipStream_t stream);
+BCG_API int bcg_gemm_w4_fp8(int epi, const void* xq, const void* wq, const float* x_scale, const float* w_scale,
+                            const void* bias, const void* residual, void* c, void* ws, void* counters, int M, int N,
+                            int K, int split_k, hipStream_t stream);
 constexpr int W4_CFG = N_CFG + 1;  // 256 x 256, four 128 x 128 waves, LDS-DMA fed (gemm_w4.hip)
 
 // Tile configurations: see CFGS (BM x BN, pipeline stages); PP_CFG = gemm_pp.hip.
@@ -445,6 +448,8 @@ BCG_API int bcg_gemm_nt_fp8(int cfg, int epi, const void* xq, const void* wq, co
                             void* counters, int M, int N, int K, int split_k, hipStream_t stream) {
   if (cfg == PP_CFG)  // the 256 x 256 ping-pong kernel's fp8 form (prefill M)
     return bcg_gemm_pp_fp8(epi, xq, wq, x_scale, w_scale, bias, residual, c, ws, counters, M, N, K, split_k, stream);
+  if (cfg == W4_CFG)  // the four-wave 256 x 256 kernel's fp8 form (32x32x64 block-scaled MFMAs)
+    return bcg_gemm_w4_fp8(epi, xq, wq, x_scale, w_scale, bias, residual, c, ws, counters, M, N, K, split_k, stream);
   if (M <= 0 || K % 128 || K <= 0 || split_k < 1 || K / 128 < split_k || !x_scale || !w_scale) return -2;
   if (split_k > 1 && (!ws || !counters)) return -2;
   if (cfg < 0 || cfg >= N_CFG || N % CFGS[cfg].bn) return -2;

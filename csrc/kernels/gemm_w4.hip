@@ -106,6 +106,7 @@ constexpr int A_BYTES = BM * 128, STAGE = A_BYTES + BN * 128;  // 64 KiB
 enum Epilogue { EPI_STORE = 0, EPI_SILU_MUL = 1, EPI_RESIDUAL = 2 };
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 static_assert(W4_RA0 + 15 * W4_RAS < W4_SLOTS && W4_DB0 + (W4_NPB - 1) * W4_DBS < W4_SLOTS &&
                   W4_RB0 + 15 * W4_RBS < W4_SLOTS,
@@ -143,16 +144,41 @@ struct SchedAlt {
                        DB0 = W4_DB0 + W4_DBS / 2, DBS = W4_DBS, RB0 = W4_RB0, RBS = W4_RBS;
   static_assert(DA0 + 7 * DAS < W4_SLOTS && DB0 + (W4_NPB - 1) * DBS < W4_SLOTS, "staggered schedule");
 };
+// fp8 (e4m3) form: a K-tile is 128 elements in the same 128-B rows; each phase = one 64-deep
+// k-step = 16 v_mfma_scale_f32_32x32x64_f8f6f4 (the cycles of 64 bf16 16x16x32), so the same
+// 16 reads and 8 pieces per phase serve twice the FLOPs.
+#ifndef W4F8_DA0
+#define W4F8_DA0 8
+#endif
+#ifndef W4F8_DB0
+#define W4F8_DB0 0
+#endif
+struct SchedF8 {
+  static constexpr int RA0 = 0, RAS = 1, DA0 = W4F8_DA0, DAS = 1, DB0 = W4F8_DB0, DBS = 2, RB0 = 0, RBS = 1;
+  static_assert(DA0 + 7 * DAS < 16 && DB0 + 7 * DBS < 16, "fp8 schedule");
+};
+struct SchedF8Alt {
+  static constexpr int RA0 = 0, RAS = 1, DA0 = W4F8_DA0 - 1, DAS = 1, DB0 = W4F8_DB0 + 1, DBS = 2, RB0 = 0, RBS = 1;
+};
+
 #ifdef W4_STAMPS
 __device__ uint64_t w4_stamps[1 << 16];  // [workgroup][wave][phase A, wait, phase B, K-tiles]
 #endif
 
-template <int EPI, bool M32>
+// M32: bf16 with v_mfma_f32_32x32x16_bf16; F8: e4m3 operands with v_mfma_scale_f32_32x32x64_f8f6f4
+// (unit E8M0 block scales; x_scale[m] * w_scale[n] applied in the epilogue)
+template <int EPI, bool M32, bool F8 = false>
 __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_w4_kernel(
-    const bf16_t* __restrict__ X, const bf16_t* __restrict__ W, const bf16_t* __restrict__ bias,
+    const void* __restrict__ Xv, const void* __restrict__ Wv, const bf16_t* __restrict__ bias,
     const bf16_t* __restrict__ residual, bf16_t* __restrict__ C, float* __restrict__ ws,
     int* __restrict__ counters, int M, int N, int K, int ldc, int inter, int m_tiles, int n_tiles,
-    int split_k) {
+    int split_k, const float* __restrict__ x_scale, const float* __restrict__ w_scale) {
+  static_assert(!F8 || (EPI != EPI_SILU_MUL && !M32), "fp8: store / residual epilogues");
+  constexpr bool L32 = M32 || F8;                      // 32x32 accumulator layout
+  constexpr int SLOTS = F8 ? 16 : W4_SLOTS;            // MFMAs per phase
+  constexpr int ESZ = F8 ? 1 : 2;                      // bytes per element
+  const unsigned char* X = static_cast<const unsigned char*>(Xv);
+  const unsigned char* W = static_cast<const unsigned char*>(Wv);
   // ONE shared array (cdna_hip_programming.md "Projection GEMM" item 4a)
   __shared__ __attribute__((aligned(1024))) unsigned char smem[W4_RING5 ? 5 * A_BYTES : 2 * STAGE];
   // LDS byte offset of tile t's X (part 0) or W (part 1) half: two 64-KiB stages, or (RING5) a
@@ -175,7 +201,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   const int gm = min(m_tiles - grp * W4_GROUP_M, W4_GROUP_M);
   const int m_tile = grp * W4_GROUP_M + in_grp % gm, n_tile = in_grp / gm;
   const int m0 = m_tile * BM, n0 = n_tile * BN;
-  const int nk_all = K / BK;
+  const int nk_all = K / (128 / ESZ);  // K-tiles of 128 B per row
   const int kt0 = split * nk_all / split_k;
   const int nk = (split + 1) * nk_all / split_k - kt0;
 
@@ -187,7 +213,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   // ---- LDS-DMA pieces: piece i (0..7) of wave w fills stage rows 32 i + 8 w + (lane >> 3),
   // physical chunk lane & 7 <- logical chunk (lane & 7) ^ ((4 w + (lane >> 4)) & 7).  Rows past
   // M / N fall outside the descriptor's range and read zeros (never stored).
-  const uint32_t row_bytes = static_cast<uint32_t>(K) * 2;
+  const uint32_t row_bytes = static_cast<uint32_t>(K) * ESZ;
   const int prow = 8 * wave + (lane >> 3);
   const int pch = ((lane & 7) ^ ((4 * wave + (lane >> 4)) & 7)) * 16;
   const i32x4 srdX = make_srd(X, static_cast<uint32_t>(M) * row_bytes);
@@ -245,12 +271,15 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   //             chunk 4 s + fq;  lane -> swizzle (fr >> 1) & 7
   //   32x32x16: f < 8 = X k-step f >> 2 (16 deep), rows wm*128 + 32 (f & 3) + (lane & 31);
   //             f >= 8 = the same for W;  chunk 4 s + 2 ks + (lane >> 5); swizzle ((lane & 31) >> 1) & 7
-  const int r_lane = M32 ? (lane & 31) : fr;
+  const int r_lane = L32 ? (lane & 31) : fr;
   const int rd_sw = (r_lane >> 1) & 7;
   const int rdA = (wm * 128 + r_lane) * 128, rdB = (wn * 128 + r_lane) * 128;
   auto read_frag = [&](int t, int s, int f, bf16x8 (&xf)[8], bf16x8 (&wf)[8]) {
     int off = slot_off(t, f >= 8) + (f < 8 ? rdA : rdB);
-    if constexpr (M32) {
+    if constexpr (F8) {  // block (f >> 1) & 3, 16-B chunk f & 1 of the lane's 32 k (k = 32 (lane >> 5) + ...)
+      const int blk = (f >> 1) & 3;
+      off += (((4 * s + 2 * (lane >> 5) + (f & 1)) ^ rd_sw) << 4) + blk * 4096;
+    } else if constexpr (M32) {
       const int ks = (f >> 2) & 1, blk = f & 3;
       off += (((4 * s + 2 * ks + (lane >> 5)) ^ rd_sw) << 4) + blk * 4096;
     } else {
@@ -264,8 +293,8 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   };
 
   // accumulators, pinned in AGPRs by the asm MFMA below: [n-block][m-block]
-  using Acc = std::conditional_t<M32, f32x16[4][4], f32x4[8][8]>;
-  constexpr int NB = M32 ? 4 : 8;
+  using Acc = std::conditional_t<L32, f32x16[4][4], f32x4[8][8]>;
+  constexpr int NB = L32 ? 4 : 8;
   Acc acc;
 #pragma unroll
   for (int i = 0; i < NB; ++i)
@@ -273,8 +302,19 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     for (int j = 0; j < NB; ++j) acc[i][j] = 0.f;
   // "memory" keeps the MFMAs in source order with the LDS reads and DMA issued between them;
   // the builtin form lets hipcc cycle the accumulators through a few AGPRs (gemm_rs.hip)
+  const int e8m0_one = 127;  // E8M0 block scale 1.0 (VGPR operand of the scaled MFMA)
   auto mf = [&](int idx, const bf16x8 (&xf)[8], const bf16x8 (&wf)[8]) {
-    if constexpr (M32) {  // idx = ks * 16 + nb * 4 + mb
+    if constexpr (F8) {  // idx = nb * 4 + mb; a block's operand = its two 16-B chunks
+      const int nb = idx >> 2, mb = idx & 3;
+      const i32x8 a = __builtin_shufflevector(__builtin_bit_cast(i32x4, wf[2 * nb]),
+                                              __builtin_bit_cast(i32x4, wf[2 * nb + 1]), 0, 1, 2, 3, 4, 5, 6, 7);
+      const i32x8 b = __builtin_shufflevector(__builtin_bit_cast(i32x4, xf[2 * mb]),
+                                              __builtin_bit_cast(i32x4, xf[2 * mb + 1]), 0, 1, 2, 3, 4, 5, 6, 7);
+      asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
+                   : "+a"(acc[nb][mb])
+                   : "v"(a), "v"(b), "v"(e8m0_one)
+                   : "memory");
+    } else if constexpr (M32) {  // idx = ks * 16 + nb * 4 + mb
       const int ks = idx >> 4, nb = (idx >> 2) & 3, mb = idx & 3;
       asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0"
                    : "+a"(acc[nb][mb])
@@ -316,7 +356,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       sX[e] = __builtin_amdgcn_readfirstlane(more ? srdX[e] : nullX[e]),
       sW[e] = __builtin_amdgcn_readfirstlane(more ? srdW[e] : nullW[e]);
 #pragma clang loop unroll(full)
-    for (int idx = 0; idx < W4_SLOTS; ++idx) {
+    for (int idx = 0; idx < SLOTS; ++idx) {
       mf(idx, x1, w1);
 #ifndef W4_ABL_NODMA
 #if W4_M0_EARLY  // M0 written one MFMA before its piece (W4_DB0 >= 1)
@@ -346,14 +386,14 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     for (int e = 0; e < 4; ++e) aX[e] = __builtin_amdgcn_readfirstlane(more_a ? srdX[e] : nullX[e]);
 #endif
 #pragma clang loop unroll(full)
-    for (int idx = 0; idx < W4_SLOTS; ++idx) {  // phase A
+    for (int idx = 0; idx < SLOTS; ++idx) {  // phase A
       mf(idx, x0, w0);
 #if W4_RING5  // X(t+2) into the slot W(t-1) left (free since the barrier of tile t-1)
       if (idx >= Sch::DA0 && (idx - Sch::DA0) % Sch::DAS == 0 && (idx - Sch::DA0) / Sch::DAS < 8)
         dma(t + 2, (idx - Sch::DA0) / Sch::DAS, aX, aX);
 #endif
 #ifdef W4_ABL_SPREAD  // timing ablation (racy): pieces 0..7 of tile t+2 issued in phase A
-      if (idx % (W4_SLOTS / 8) == 2) dma(t + 2, idx / (W4_SLOTS / 8), srdX, srdW);
+      if (idx % (SLOTS / 8) == 2) dma(t + 2, idx / (SLOTS / 8), srdX, srdW);
 #endif
 #ifndef W4_ABL_NOREAD
       if (idx >= Sch::RA0 && (idx - Sch::RA0) % Sch::RAS == 0 && (idx - Sch::RA0) / Sch::RAS < 16)
@@ -385,14 +425,21 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   }
 #endif
   };
+  if constexpr (F8) {
+    if (W4_STAGGER && (wave & 1))
+      run(SchedF8Alt{});
+    else
+      run(SchedF8{});
+  } else {
 #if W4_STAGGER
-  if (wave & 1)
-    run(SchedAlt{});
-  else
-    run(SchedMain{});
+    if (wave & 1)
+      run(SchedAlt{});
+    else
+      run(SchedMain{});
 #else
-  run(SchedMain{});
+    run(SchedMain{});
 #endif
+  }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   // the last MFMAs' results are read by VALU / stores below: cover the MFMA D -> read hazard
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
@@ -404,8 +451,8 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   //             registers 4 g + e;  i = 4 nb + g (g = 0..3)
   // value(nb, mb) returns the block's registers (accumulators, or the split-K slab sum).
   auto epilogue = [&](auto value) {
-    constexpr int MB = M32 ? 32 : 16;
-    const int ml = M32 ? (lane & 31) : fr;
+    constexpr int MB = L32 ? 32 : 16;
+    const int ml = L32 ? (lane & 31) : fr;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const int m = m0 + wm * 128 + j * MB + ml;
@@ -413,7 +460,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
         const auto blk = value(nb, j);
-        constexpr int NG = M32 ? 4 : 1;  // quads per block
+        constexpr int NG = L32 ? 4 : 1;  // quads per block
         if constexpr (EPI == EPI_SILU_MUL) {
           // 16-row blocks of the tile alternate gate / up of the same 16 features:
           //   16x16x32: block pairs (nb, nb+1);  32x32x16: quads g and g + 2 of one block
@@ -434,9 +481,15 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         } else {
 #pragma unroll
           for (int g = 0; g < NG; ++g) {
-            const int n = n0 + wn * 128 + (M32 ? nb * 32 + 8 * g + 4 * (lane >> 5) : nb * 16 + 4 * fq);
+            const int n = n0 + wn * 128 + (L32 ? nb * 32 + 8 * g + 4 * (lane >> 5) : nb * 16 + 4 * fq);
             if (n >= N) continue;
             float v[4] = {blk[4 * g], blk[4 * g + 1], blk[4 * g + 2], blk[4 * g + 3]};
+            if constexpr (F8) {  // dequantise: row scale x column scales
+              const float xs = x_scale[m];
+              const f32x4 wsc = *reinterpret_cast<const f32x4*>(w_scale + n);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] *= xs * wsc[e];
+            }
             if (bias != nullptr) {
               const u16x4 b = *reinterpret_cast<const u16x4*>(bias + n);
 #pragma unroll
@@ -462,7 +515,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   // all the slabs (its own included) straight into the epilogue -- the accumulators die at
   // the store, so the reduction needs no second register copy of the tile.  Slab layout: per
   // (wave, block, 16-B quarter) 256 floats, lane-major (any layout both sides agree on).
-  constexpr int QPB = M32 ? 4 : 1;  // 16-B quarters per block per lane
+  constexpr int QPB = L32 ? 4 : 1;  // 16-B quarters per block per lane
   float* slab = ws + static_cast<size_t>(tile) * split_k * (BM * BN);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, split_k * BM * BN * 4, 0x00020000);
   __syncthreads();  // every wave is past its last ds_read: smem is reusable as the flag slot
@@ -505,15 +558,15 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   });
 }
 
-template <int EPI>
+template <int EPI, bool F8 = false>
 int launch_w4(const void* x, const void* w, const void* bias, const void* res, void* c, float* ws, int* cnt, int M,
-              int N, int K, int inter, int split_k, hipStream_t stream) {
+              int N, int K, int inter, int split_k, hipStream_t stream, const float* xs = nullptr,
+              const float* wsc = nullptr) {
   const int m_tiles = (M + BM - 1) / BM, n_tiles = (N + BN - 1) / BN;
   const int ldc = EPI == EPI_SILU_MUL ? inter : N;
-  hipLaunchKernelGGL((gemm_w4_kernel<EPI, W4_MFMA32 != 0>), dim3(m_tiles * n_tiles * split_k), dim3(256), 0, stream,
-                     static_cast<const bf16_t*>(x), static_cast<const bf16_t*>(w), static_cast<const bf16_t*>(bias),
-                     static_cast<const bf16_t*>(res), static_cast<bf16_t*>(c), ws, cnt, M, N, K, ldc, inter, m_tiles,
-                     n_tiles, split_k);
+  hipLaunchKernelGGL((gemm_w4_kernel<EPI, !F8 && W4_MFMA32 != 0, F8>), dim3(m_tiles * n_tiles * split_k), dim3(256),
+                     0, stream, x, w, static_cast<const bf16_t*>(bias), static_cast<const bf16_t*>(res),
+                     static_cast<bf16_t*>(c), ws, cnt, M, N, K, ldc, inter, m_tiles, n_tiles, split_k, xs, wsc);
   return BCG_CHECK_LAUNCH();
 }
 
@@ -546,6 +599,30 @@ BCG_API int bcg_gemm_w4(int epi, const void* x, const void* w, const void* bias,
     case EPI_RESIDUAL:
       if (!residual) return -2;
       return launch_w4<EPI_RESIDUAL>(x, w, bias, residual, c, wsf, cnt, M, N, K, inter, split_k, stream);
+    default: return -2;
+  }
+}
+
+// fp8 (e4m3fn) projection: C = x_scale[m] * w_scale[n] * (Xq . Wq^T) (+ bias) (+ residual).
+// epi: 0 = store, 2 = residual + result.  K % 128 == 0, K/128 >= split_k; N % 16 == 0 (a partial
+// last n-tile is masked); x_scale [M] / w_scale [N] fp32; split-K workspace as bcg_gemm_w4.
+BCG_API int bcg_gemm_w4_fp8(int epi, const void* xq, const void* wq, const float* x_scale, const float* w_scale,
+                            const void* bias, const void* residual, void* c, void* ws, void* counters, int M, int N,
+                            int K, int split_k, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || N % 16 || K % 128 || K <= 0 || split_k < 1 || K / 128 < split_k) return -2;
+  if (!x_scale || !w_scale) return -2;
+  if (1ull * (M + BM) * K >= (1ull << 31) || 1ull * (N + BN) * K >= (1ull << 31)) return -2;
+  if (split_k > 1 && (!ws || !counters)) return -2;
+  float* wsf = static_cast<float*>(ws);
+  int* cnt = static_cast<int*>(counters);
+  switch (epi) {
+    case EPI_STORE:
+      return launch_w4<EPI_STORE, true>(xq, wq, bias, residual, c, wsf, cnt, M, N, K, 0, split_k, stream, x_scale,
+                                        w_scale);
+    case EPI_RESIDUAL:
+      if (!residual) return -2;
+      return launch_w4<EPI_RESIDUAL, true>(xq, wq, bias, residual, c, wsf, cnt, M, N, K, 0, split_k, stream,
+                                           x_scale, w_scale);
     default: return -2;
   }
 }

@@ -193,17 +193,19 @@ def test_linear_fp8_dispatch_matches_library(hip):
 @pytest.mark.parametrize("M,N,K,split", [(300, 1040, 128, 1), (2048 + 77, 1536, 1024, 1), (1, 4112, 384, 1),
                                          (513, 784, 1024, 3), (4096, 6144, 2048, 1)])
 @pytest.mark.parametrize("epi", [0, 2])
-def test_gemm_pp_fp8(hip, M, N, K, split, epi):
-    """The 256x256 ping-pong kernel's fp8 form (cfg 10, block-scaled K = 128 MFMAs): edges
-    (1-3 K-tiles, partial tiles in M and N), split-K, residual epilogue, repeated launches."""
+@pytest.mark.parametrize("cfg", [10, 11])
+def test_gemm_pp_fp8(hip, M, N, K, split, epi, cfg):
+    """The 256x256 kernels' fp8 forms (cfg 10 ping-pong: 16x16x128 block-scaled MFMAs; cfg 11
+    four-wave: 32x32x64): edges (1-3 K-tiles, partial tiles in M and N), split-K, residual
+    epilogue, repeated launches."""
     xq, xs, wq, ws, ref = _fp8_operands(M, N, K, M + N + K + epi)
     b = torch.randn(N, device="cuda").to(torch.bfloat16)
     for _ in range(2):
         if epi == 2:
             r = torch.randn(M, N, device="cuda").to(torch.bfloat16)
             want = ref + r.float() + b.float()
-            got = hip.gemm_nt_fp8(xq, xs, wq, ws, (10, split), 2, bias=b, residual=r, out=r)
+            got = hip.gemm_nt_fp8(xq, xs, wq, ws, (cfg, split), 2, bias=b, residual=r, out=r)
         else:
             want = ref + b.float()
-            got = hip.gemm_nt_fp8(xq, xs, wq, ws, (10, split), 0, bias=b)
+            got = hip.gemm_nt_fp8(xq, xs, wq, ws, (cfg, split), 0, bias=b)
         _close(got, want)

@@ -1,5 +1,5 @@
 """fp8 projection GEMMs: every hand fp8 tile x split-K vs hipBLASLt (_scaled_mm); at prefill M
-(> 1024) only the 256x256 ping-pong kernel (cfg 10).
+(> 1024) only the 256x256 kernels (cfg 10 ping-pong, cfg 11 four-wave).
 
   python tools/bench_fp8_gemm.py [--model mistral-22b] [--ms 32,64,128,160,256,320,512]
 
@@ -63,9 +63,9 @@ def main():
                 return torch._scaled_mm(xq, wq.t(), scale_a=xs.view(-1, 1), scale_b=wsc.view(1, -1),
                                         out_dtype=torch.bfloat16)
             res = {"lib": timed(lib)}
-            for c in range(11):  # 10 = the 256 x 256 ping-pong kernel (N % 16)
+            for c in range(12):  # 10 / 11 = the 256 x 256 ping-pong / four-wave kernels (N % 16)
                 bm, bn = hip.gemm_plan.tiles[c]
-                if N % (16 if c == 10 else bn) or (M > 1024 and c != 10):
+                if N % (16 if c >= 10 else bn) or (M > 1024 and c < 10):
                     continue
                 for sk in (1, 2, 3, 4, 6):
                     if K // 128 < sk or (M > 1024 and sk > 1):

@@ -32,8 +32,8 @@ step() {  # name limit command...
 
 case "$cmd" in
   tests)
-    step "tests/$TAG" "${LIMIT:-1100}" python -u -m pytest -x -q --timeout 120 --timeout-method thread \
-      ${@:-tests -m gpu}
+    [ $# -gt 0 ] || set -- tests -m gpu
+    step "tests/$TAG" "${LIMIT:-1100}" python -u -m pytest -x -q --timeout 120 --timeout-method thread "$@"
     ;;
   bench)
     mkdir -p gpurun_out/bench
