@@ -91,7 +91,7 @@
 #endif
 #define W4_NPB (W4_RING5 ? 8 : W4_ABL_NPIECE)  // pieces issued in phase B
 #ifndef W4_STAGGER
-#define W4_STAGGER 0  // 1: odd waves run the loop with their pieces half a stride later
+#define W4_STAGGER 1  // odd waves run the loop with their pieces half a stride later (+0.4-1 %, profiles/r4_gemm_w4)
 #endif
 #ifndef W4_M0_EARLY
 #define W4_M0_EARLY 0  // 1: each piece's M0 write one MFMA ahead of the piece (needs W4_DB0 >= 1)
