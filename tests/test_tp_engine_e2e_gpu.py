@@ -133,8 +133,9 @@ def test_tp2_engine_plays_bcg_rounds(tmp_path, model, quant, honest, byz):
         assert drv["counters"]["votes_accepted"] >= 0.8 * n * played, drv
         assert drv["captures"] > 0, drv                                      # decode ran in HIP graphs
         assert drv["hand_calls"] > 0
-        # no decode-bucket projection (M <= 1024) of an untuned shape falls to the library
-        assert not drv["untuned"], drv["untuned"]
+        # no decode-bucket projection (M <= 1024) of an untuned TP shard shape falls to the library
+        # (the TP = 1 reference of Qwen3-32B is not a BASELINE configuration: its shapes are untuned)
+        assert world == 1 or not drv["untuned"], drv["untuned"]
     d1, d2 = runs[1][0], runs[2][0]
     assert d1["keys"] == d2["keys"]                   # same statistics payload
     follower = runs[2][1]
