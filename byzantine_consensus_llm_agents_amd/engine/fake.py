@@ -260,6 +260,9 @@ class HostModelBackend:
         self.lock = threading.Lock()
         self.free_at = 0.0
         self.stats = {"prompt_tokens": 0, "cached_tokens": 0, "generated_tokens": 0, "calls": 0}
+        self.in_flight = 0
+        self.closing = threading.Event()
+        self.idle = threading.Condition(self.lock)
 
     def _answer(self, prompt: str, schema: Optional[Dict]) -> str:
         if schema and "decision" in schema.get("properties", {}):
@@ -267,12 +270,22 @@ class HostModelBackend:
         return self.burn._answer(prompt, schema)
 
     def generate(self, prompts, params_list):
+        import threading
         import time
+        if self.closing.is_set():  # after shutdown: park the (daemon) caller in Python, not in native code
+            threading.Event().wait()
         t0 = time.perf_counter()
-        schemas = [p.guided_decoding.json if p.guided_decoding is not None else None for p in params_list]
-        p_ids = self.tok.encode_batch(list(prompts))
-        out_ids = self.tok.encode_batch([self._answer(p, s) for p, s in zip(prompts, schemas)])
-        texts = [self.tok.decode(ids) for ids in out_ids]
+        with self.lock:
+            self.in_flight += 1
+        try:
+            schemas = [p.guided_decoding.json if p.guided_decoding is not None else None for p in params_list]
+            p_ids = self.tok.encode_batch(list(prompts))
+            out_ids = self.tok.encode_batch([self._answer(p, s) for p, s in zip(prompts, schemas)])
+            texts = [self.tok.decode(ids) for ids in out_ids]
+        finally:
+            with self.lock:
+                self.in_flight -= 1
+                self.idle.notify_all()
         n_prompt = sum(len(i) for i in p_ids)
         n_cached = int(self.cached_frac * n_prompt)
         n_gen = sum(len(i) for i in out_ids)
@@ -290,4 +303,8 @@ class HostModelBackend:
         return texts
 
     def shutdown(self):
-        pass
+        # no caller may still be inside the tokenizer's native code when the interpreter
+        # finalizes: a daemon thread unwound there aborts the process
+        self.closing.set()
+        with self.lock:
+            self.idle.wait_for(lambda: self.in_flight == 0, timeout=60.0)
