@@ -91,26 +91,31 @@ int main(int argc, char** argv) {
   float ms = 0;
   CK(hipEventElapsedTime(&ms, a, b));
   const double us = ms * 1e3 / iters;
-  char extra[256] = "";
+  char extra[512] = "";
 #ifdef W4_STAMPS
-  {  // per-wave cycles per K-tile of the last launch: medians over the stamped waves
-    std::vector<uint64_t> st(1 << 16);
+  {  // per-wave cycles per K-tile of the last launch: medians over the stamped waves, and the
+     // share of each wave's lifetime spent outside the K-loop (epilogues, prologue)
+    std::vector<uint64_t> st(1 << 17);
     CK(hipDeviceSynchronize());
-    if (bcg_gemm_w4_stamps(st.data(), 1 << 16) == 0) {
+    if (bcg_gemm_w4_stamps(st.data(), 1 << 17) == 0) {
       const int nw = std::min(tiles * split, 4096) * 4;
-      std::vector<double> a, wt, b;
+      std::vector<double> a, wt, b, e, other;
       for (int i = 0; i < nw; ++i) {
-        const uint64_t* e = &st[i * 4];
-        if (!e[3]) continue;
-        a.push_back((double)e[0] / e[3]), wt.push_back((double)e[1] / e[3]), b.push_back((double)e[2] / e[3]);
+        const uint64_t* s8 = &st[i * 8];
+        if (!s8[3]) continue;
+        a.push_back((double)s8[0] / s8[3]), wt.push_back((double)s8[1] / s8[3]), b.push_back((double)s8[2] / s8[3]);
+        e.push_back((double)s8[4] / s8[6]);
+        other.push_back(1.0 - (double)(s8[0] + s8[1] + s8[2]) / s8[5]);
       }
       auto med = [](std::vector<double>& v) {
         if (v.empty()) return 0.0;
         std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
         return v[v.size() / 2];
       };
-      snprintf(extra, sizeof extra, ", \"cyc_per_ktile\": {\"phaseA\": %.0f, \"wait_barrier\": %.0f, \"phaseB\": %.0f}",
-               med(a), med(wt), med(b));
+      snprintf(extra, sizeof extra,
+               ", \"cyc_per_ktile\": {\"phaseA\": %.0f, \"wait_barrier\": %.0f, \"phaseB\": %.0f}, "
+               "\"cyc_per_epilogue\": %.0f, \"frac_outside_kloop\": %.3f",
+               med(a), med(wt), med(b), med(e), med(other));
     }
   }
 #endif

@@ -36,6 +36,7 @@
 // swizzle is applied to each lane's SOURCE chunk.  Operands swapped in the MFMA (W fragment
 // as A) so a lane holds 4 consecutive output columns of one row.  XCD-aware grouped tile
 // order and last-arriver split-K as gemm_pp.hip; the same host contract (bcg_gemm_w4).
+#include <algorithm>
 #include <type_traits>
 
 #include "common.h"
@@ -90,6 +91,15 @@
 #define W4_ABL_PIECE0 0
 #endif
 #define W4_NPB (W4_RING5 ? 8 : W4_ABL_NPIECE)  // pieces issued in phase B
+#ifndef W4_RES_PF
+#define W4_RES_PF 0  // residual tile -> L2 over an item's last N K-tiles (N % 4 == 0); measured: no gain
+#endif
+#ifndef W4_NT_STORE
+#define W4_NT_STORE 0  // non-temporal output stores; measured: 3-6 % slower
+#endif
+#ifndef W4_PERSIST
+#define W4_PERSIST 1  // one workgroup per CU streaming its tiles (split_k == 1; profiles/r4_gemm_w4)
+#endif
 #ifndef W4_STAGGER
 #define W4_STAGGER 1  // odd waves run the loop with their pieces half a stride later (+0.4-1 %, profiles/r4_gemm_w4)
 #endif
@@ -162,7 +172,8 @@ struct SchedF8Alt {
 };
 
 #ifdef W4_STAMPS
-__device__ uint64_t w4_stamps[1 << 16];  // [workgroup][wave][phase A, wait, phase B, K-tiles]
+// [workgroup][wave][phase A, wait, phase B, K-tiles, epilogues, kernel total, items, -]
+__device__ uint64_t w4_stamps[1 << 17];
 #endif
 
 // M32: bf16 with v_mfma_f32_32x32x16_bf16; F8: e4m3 operands with v_mfma_scale_f32_32x32x64_f8f6f4
@@ -190,20 +201,35 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       return static_cast<uint32_t>(t & 1) * STAGE + part * A_BYTES;
   };
 
-  // ---- XCD-aware order (bijective remap), grouped m-tiles, then (tile, k-split) ----
+  // ---- work items: nwg = tiles x k-splits.  A persistent launch (gridDim.x < nwg, split_k == 1
+  // only) gives workgroup b the items b, b + G, b + 2G, ...: one continuous stream of K-tiles in
+  // which the next item's first tiles are already in flight while this item's epilogue runs.
+  // Item -> tile: XCD-aware bijective remap (item i runs on XCD i % 8 when G % 8 == 0, so each
+  // XCD's CUs walk one contiguous range of remapped ids), grouped m-tiles, then (tile, k-split).
   const int nwg = m_tiles * n_tiles * split_k;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, rem = nwg & 7;
-  const int r_id = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (bid >> 3);
-  const int split = r_id % split_k;
-  const int tile = r_id / split_k;
-  const int grp = tile / (W4_GROUP_M * n_tiles), in_grp = tile % (W4_GROUP_M * n_tiles);
-  const int gm = min(m_tiles - grp * W4_GROUP_M, W4_GROUP_M);
-  const int m_tile = grp * W4_GROUP_M + in_grp % gm, n_tile = in_grp / gm;
-  const int m0 = m_tile * BM, n0 = n_tile * BN;
+  const int G = gridDim.x;
+  const int n_items = (nwg - 1 - static_cast<int>(blockIdx.x)) / G + 1;
+  struct Geo {
+    int m0, n0, tile, split;
+  };
+  auto geo = [&](int j) {
+    const int i = blockIdx.x + j * G;
+    const int xcd = i & 7, q = nwg >> 3, rem = nwg & 7;
+    const int r_id = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (i >> 3);
+    Geo g;
+    g.split = r_id % split_k;
+    g.tile = r_id / split_k;
+    const int grp = g.tile / (W4_GROUP_M * n_tiles), in_grp = g.tile % (W4_GROUP_M * n_tiles);
+    const int gm = min(m_tiles - grp * W4_GROUP_M, W4_GROUP_M);
+    g.m0 = (grp * W4_GROUP_M + in_grp % gm) * BM;
+    g.n0 = (in_grp / gm) * BN;
+    return g;
+  };
+  Geo gc = geo(0);                     // the item whose accumulators are live
   const int nk_all = K / (128 / ESZ);  // K-tiles of 128 B per row
-  const int kt0 = split * nk_all / split_k;
-  const int nk = (split + 1) * nk_all / split_k - kt0;
+  const int kt0 = gc.split * nk_all / split_k;
+  const int nk = (gc.split + 1) * nk_all / split_k - kt0;  // (all items alike: split_k == 1 when persistent)
+  const int total = n_items * nk;                           // K-tiles of the stream
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -212,18 +238,22 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 
   // ---- LDS-DMA pieces: piece i (0..7) of wave w fills stage rows 32 i + 8 w + (lane >> 3),
   // physical chunk lane & 7 <- logical chunk (lane & 7) ^ ((4 w + (lane >> 4)) & 7).  Rows past
-  // M / N fall outside the descriptor's range and read zeros (never stored).
+  // M / N fall outside the descriptor's range and read zeros (never stored).  Each item's
+  // descriptors start at its first X / W row, so the lane offsets are the same for every item.
   const uint32_t row_bytes = static_cast<uint32_t>(K) * ESZ;
   const int prow = 8 * wave + (lane >> 3);
   const int pch = ((lane & 7) ^ ((4 * wave + (lane >> 4)) & 7)) * 16;
-  const i32x4 srdX = make_srd(X, static_cast<uint32_t>(M) * row_bytes);
-  const i32x4 srdW = make_srd(W, static_cast<uint32_t>(EPI == EPI_SILU_MUL ? 2 * inter : N) * row_bytes);
-  const uint32_t voffX = static_cast<uint32_t>(m0 + prow) * row_bytes + pch;
+  const int w_rows = EPI == EPI_SILU_MUL ? 2 * inter : N;
+  auto item_srd = [&](const Geo& g, i32x4& sX, i32x4& sW) {
+    const int wr0 = EPI == EPI_SILU_MUL ? (g.n0 >> 1) : g.n0;
+    sX = make_srd(X + static_cast<size_t>(g.m0) * row_bytes, static_cast<uint32_t>(M - g.m0) * row_bytes);
+    sW = make_srd(W + static_cast<size_t>(wr0) * row_bytes, static_cast<uint32_t>(w_rows - wr0) * row_bytes);
+  };
+  const uint32_t voffX = static_cast<uint32_t>(prow) * row_bytes + pch;
   // SILU: 16-row blocks of the tile alternate gate / up of the same 16 features, so stage row
   // 32 i + r (r < 32) holds W row (r >> 4) * inter + n0/2 + 16 i + (r & 15)
   const uint32_t voffW =
-      static_cast<uint32_t>(EPI == EPI_SILU_MUL ? (wave >> 1) * inter + (n0 >> 1) + (prow & 15) : n0 + prow) *
-          row_bytes + pch;
+      static_cast<uint32_t>(EPI == EPI_SILU_MUL ? (wave >> 1) * inter + (prow & 15) : prow) * row_bytes + pch;
   const uint32_t strideX = 32u * row_bytes;
   const uint32_t strideW = (EPI == EPI_SILU_MUL ? 16u : 32u) * row_bytes;
   // the row part of a piece's offset stays in the VGPR offset: only that is range-checked
@@ -232,13 +262,14 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 #pragma unroll
   for (int i = 0; i < 8; ++i) vX[i] = voffX + i * strideX, vW[i] = voffW + i * strideW;
   const uint32_t lds_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(smem));
-  // piece q (0..15) of tile t into `stage`: q < 8 X piece q, else W piece q - 8
+  // piece q (0..15) of stream tile t: q < 8 X piece q, else W piece q - 8
   auto dma_m0 = [&](int t, int q) {
     return __builtin_amdgcn_readfirstlane(lds_base + slot_off(t, q >= 8) + (q & 7) * 4096 + wave * 1024);
   };
-  // mode 0: M0 write + piece in one statement; 1: the piece only (M0 set earlier: set_m0)
-  auto dma = [&](int t, int q, const i32x4& sX, const i32x4& sW, int mode = 0) {
-    const uint32_t kb = static_cast<uint32_t>(kt0 + t) * (BK * 2);
+  // stream tile t = K-tile kt of its item; mode 0: M0 write + piece in one statement; 1: the
+  // piece only (M0 set earlier: set_m0)
+  auto dma = [&](int t, int kt, int q, const i32x4& sX, const i32x4& sW, int mode = 0) {
+    const uint32_t kb = static_cast<uint32_t>(kt0 + kt) * (BK * 2);
     const bool isx = q < 8;
     const int i = q & 7;
     const uint32_t soff = __builtin_amdgcn_readfirstlane(kb);
@@ -329,32 +360,192 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   };
 
   bf16x8 x0[8], w0[8], x1[8], w1[8];
-  // ---- prologue: tiles 0 and 1 in flight, tile 0 landed, k-step 0 of tile 0 in registers ----
+  // DMA cursor: stream tile t + 2 is K-tile ktd of item jd, whose descriptors are dX / dW
+  i32x4 dX, dW;
+  item_srd(gc, dX, dW);
+  i32x4 nullX = dX, nullW = dW;  // zero-range descriptors: pieces past the stream's last tile
+  nullX[2] = 0, nullW[2] = 0;
+  int jd = 0, ktd = 0;
+  auto advance = [&]() {
+    if (++ktd == nk) {
+      ktd = 0;
+      if (++jd < n_items) item_srd(geo(jd), dX, dW);
+    }
+  };
+  // ---- prologue: stream tiles 0 and 1 in flight, tile 0 landed, k-step 0 of tile 0 in registers ----
 #pragma unroll
-  for (int q = 0; q < 16; ++q) dma(0, q, srdX, srdW);
-  if (nk > 1) {
+  for (int q = 0; q < 16; ++q) dma(0, 0, q, dX, dW);
+  advance();
+  if (total > 1) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) dma(1, q, srdX, srdW);
+    for (int q = 0; q < 16; ++q) dma(1, ktd, q, dX, dW);
     asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
 #pragma unroll
   for (int f = 0; f < 16; ++f) read_frag(0, 0, f, x0, w0);
-  i32x4 nullX = srdX, nullW = srdW;  // zero-range descriptors: pieces past the last tile
-  nullX[2] = 0, nullW[2] = 0;
 
-  // phase B of tile t.  Past the last tile the pieces go through a zero-range descriptor: no
-  // memory traffic, the zeros land in a stage nobody reads -- branch-free, one body (a
-  // branch around the pieces, or two copies of the phase, made hipcc spill the accumulators)
-  auto phase_b = [&](int t, int cur, auto sch) {
-    using Sch = decltype(sch);
-    const bool more = t + 2 < nk;
-    i32x4 sX, sW;
+  // ---- epilogue of item g.  The tile is seen as [n-group][m-block] quads of 4 consecutive output
+  // columns (n) of one row (m) per lane: q = quad(i, j) with i over 32 n-groups, j over NB m-blocks.
+  //   16x16x32: block (nb, mb) lane: D[n = 16 nb + 4 fq + e][m = 16 mb + fr];  i = nb
+  //   32x32x16: block (nb, mb) lane: D[n = 32 nb + 8 g + 4 (lane >> 5) + e][m = 32 mb + (lane & 31)],
+  //             registers 4 g + e;  i = 4 nb + g (g = 0..3)
+  // value(nb, mb) returns the block's registers (accumulators, or the split-K slab sum).
+  auto epilogue = [&](const Geo& geo_c, auto value) {
+    constexpr int MB = L32 ? 32 : 16;
+    constexpr int NG = L32 ? 4 : 1;  // quads per block
+    // the lane index re-enters here through an opaque move: the epilogue's per-lane address
+    // math cannot be hoisted out of the K-loop (it would hold ~100 VGPRs across it and spill)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int fr = ln & 15, fq = ln >> 4;
+    const int ml = L32 ? (ln & 31) : fr;
+    const int m0 = geo_c.m0, n0 = geo_c.n0;
+    auto row = [&](int j) { return m0 + wm * 128 + j * MB + ml; };
+    auto st4 = [&](bf16_t* p, u16x4 v) {
+#if W4_NT_STORE  // streaming stores: the output tile does not displace the operand panels in L2
+      __builtin_nontemporal_store(v, reinterpret_cast<u16x4*>(p));
+#else
+      *reinterpret_cast<u16x4*>(p) = v;
+#endif
+    };
+    if constexpr (EPI == EPI_SILU_MUL) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      sX[e] = __builtin_amdgcn_readfirstlane(more ? srdX[e] : nullX[e]),
-      sW[e] = __builtin_amdgcn_readfirstlane(more ? srdW[e] : nullW[e]);
+      for (int j = 0; j < NB; ++j) {
+        const int m = row(j);
+        if (m >= M) continue;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          const auto blk = value(nb, j);
+          // 16-row blocks of the tile alternate gate / up of the same 16 features:
+          //   16x16x32: block pairs (nb, nb+1);  32x32x16: quads g and g + 2 of one block
+          if constexpr (M32) {
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+              const int feat = (n0 >> 1) + wn * 64 + nb * 16 + 8 * g + 4 * (ln >> 5);
+              st4(C + static_cast<size_t>(m) * ldc + feat,
+                  pack4(silu(blk[4 * g]) * blk[4 * g + 8], silu(blk[4 * g + 1]) * blk[4 * g + 9],
+                        silu(blk[4 * g + 2]) * blk[4 * g + 10], silu(blk[4 * g + 3]) * blk[4 * g + 11]));
+            }
+          } else if (nb % 2 == 0) {
+            const auto u = value(nb + 1, j);
+            const int feat = (n0 >> 1) + wn * 64 + (nb >> 1) * 16 + 4 * fq;
+            st4(C + static_cast<size_t>(m) * ldc + feat,
+                pack4(silu(blk[0]) * u[0], silu(blk[1]) * u[1], silu(blk[2]) * u[2], silu(blk[3]) * u[3]));
+          }
+          // one block at a time: hoisting every accumulator read ahead of the stores would need
+          // the whole tile in VGPRs
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else {
+      // batches of JG m-blocks; the residual quads of the next batch are loaded before this
+      // batch is computed (one HBM round trip per batch, overlapped, instead of one per quad)
+      constexpr int JG = L32 ? 1 : 2;
+      constexpr int NQ = NB * NG;  // quads per m-block per lane
+      auto col = [&](int q) {
+        const int nb = q / NG, g = q % NG;
+        return n0 + wn * 128 + (L32 ? nb * 32 + 8 * g + 4 * (ln >> 5) : nb * 16 + 4 * fq);
+      };
+      // Every load is unconditional (addresses clamped into the tensor) and always consumed; only
+      // the stores are masked.  A load whose result a masked path skipped would still be pending
+      // at the K-loop's back edge, and hipcc's wait for it there (vmcnt(0) at the top of every
+      // K-tile) would drain the LDS-DMA pieces in flight.
+      auto mcl = [&](int m) { return m < M ? m : M - 1; };
+      auto ncl = [&](int n) { return n < N ? n : N - 4; };
+      u16x4 rr[2][JG][NQ];
+      auto load_batch = [&](int bf, int j0) {
+        if constexpr (EPI == EPI_RESIDUAL) {
+#pragma unroll
+          for (int jj = 0; jj < JG; ++jj)
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+              rr[bf][jj][q] = *reinterpret_cast<const u16x4*>(residual + static_cast<size_t>(mcl(row(j0 + jj))) * ldc +
+                                                             ncl(col(q)));
+        }
+      };
+      // (fp8: its scale loads need those registers -- residual quads are loaded where used)
+      if (!F8) load_batch(0, 0);
+#pragma unroll
+      for (int j0 = 0; j0 < NB; j0 += JG) {
+        const int bf = (j0 / JG) & 1;
+        if (!F8 && j0 + JG < NB) load_batch(bf ^ 1, j0 + JG);
+#pragma unroll
+        for (int jj = 0; jj < JG; ++jj) {
+          const int j = j0 + jj, m = row(j);
+          if (F8 && m >= M) continue;  // (fp8: no residual batch; masked rows skip their scale loads)
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) {
+            const auto blk = value(nb, j);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+              const int q = nb * NG + g, n = col(q);
+              if (F8 && n >= N) continue;
+              float v[4] = {blk[4 * g], blk[4 * g + 1], blk[4 * g + 2], blk[4 * g + 3]};
+              if constexpr (F8) {  // dequantise: row scale x column scales
+                const float xs = x_scale[m];
+                const f32x4 wsc = *reinterpret_cast<const f32x4*>(w_scale + n);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] *= xs * wsc[e];
+              }
+              if (bias != nullptr) {
+                const u16x4 b = *reinterpret_cast<const u16x4*>(bias + ncl(n));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] += bf2f(b[e]);
+              }
+              if constexpr (EPI == EPI_RESIDUAL) {
+                const u16x4 r4 =
+                    F8 ? *reinterpret_cast<const u16x4*>(residual + static_cast<size_t>(m) * ldc + n) : rr[bf][jj][q];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] += bf2f(r4[e]);
+              }
+              if (m < M && n < N) st4(C + static_cast<size_t>(m) * ldc + n, pack4(v[0], v[1], v[2], v[3]));
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
+  // accumulator block -> VGPRs through explicit reads: the accumulators then have no use outside
+  // asm AGPR operands inside the loop (a plain copy there lets hipcc re-class them and spill)
+  auto read_acc = [&](const auto& a) {
+    std::remove_cv_t<std::remove_reference_t<decltype(a)>> r;
+#pragma unroll
+    for (int e = 0; e < (L32 ? 16 : 4); ++e) {
+      float v;
+      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v) : "a"(a[e]));
+      r[e] = v;
+    }
+    return r;
+  };
+  // the accumulators restart at zero for the next item: MFMAs of zero operands with an inline-0
+  // accumulator write them in place (a plain `acc = 0` makes hipcc route the zeros through
+  // VGPRs and spill across the loop)
+  auto zero_acc = [&]() {
+    // (z's VALU writes -> the MFMAs' reads need wait states that hipcc does not insert before
+    // inline asm: without them the first MFMAs read stale registers)
+    bf16x8 z = {};
+    asm volatile("s_nop 4" : "+v"(z));
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        if constexpr (L32)
+          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %1, 0" : "=a"(acc[i][j]) : "v"(z) : "memory");
+        else
+          asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %1, 0" : "=a"(acc[i][j]) : "v"(z) : "memory");
+      }
+  };
+
+  // phase B of stream tile t (W pieces of tile t + 2 = K-tile kt2 of its item).  Past the last
+  // tile the pieces go through a zero-range descriptor: no memory traffic, the zeros land in a
+  // stage nobody reads -- branch-free, one body (a branch around the pieces, or two copies of
+  // the phase, made hipcc spill the accumulators)
+  auto phase_b = [&](int t, int kt2, const i32x4& sX, const i32x4& sW, auto sch) {
+    using Sch = decltype(sch);
 #pragma clang loop unroll(full)
     for (int idx = 0; idx < SLOTS; ++idx) {
       mf(idx, x1, w1);
@@ -364,7 +555,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         set_m0(t + 2, (idx + 1 - Sch::DB0) / Sch::DBS + W4_ABL_PIECE0 + (W4_RING5 ? 8 : 0));
 #endif
       if (idx >= Sch::DB0 && (idx - Sch::DB0) % Sch::DBS == 0 && (idx - Sch::DB0) / Sch::DBS < W4_NPB)
-        dma(t + 2, (idx - Sch::DB0) / Sch::DBS + W4_ABL_PIECE0 + (W4_RING5 ? 8 : 0), sX, sW, W4_M0_EARLY);
+        dma(t + 2, kt2, (idx - Sch::DB0) / Sch::DBS + W4_ABL_PIECE0 + (W4_RING5 ? 8 : 0), sX, sW, W4_M0_EARLY);
 #endif
 #ifndef W4_ABL_NOREAD
       if (idx >= Sch::RB0 && (idx - Sch::RB0) % Sch::RBS == 0 && (idx - Sch::RB0) / Sch::RBS < 16)
@@ -374,55 +565,93 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   };
   auto run = [&](auto sch) {
     using Sch = decltype(sch);
-#ifdef W4_STAMPS  // diagnostic build: per-wave cycles in phase A / the wait + barrier / phase B
-  uint64_t cyc_a = 0, cyc_w = 0, cyc_b = 0, t_end = __builtin_amdgcn_s_memtime();
+    int ktc = 0, jc = 0;  // the live item's K-tile count and index
+    int pf_sink = 0;      // (W4_RES_PF)
+#ifdef W4_STAMPS  // diagnostic build: per-wave cycles in phase A / the wait + barrier / phase B / epilogues
+    const uint64_t t_start = __builtin_amdgcn_s_memtime();
+    uint64_t cyc_a = 0, cyc_w = 0, cyc_b = 0, cyc_e = 0, t_end = t_start;
 #endif
-  for (int t = 0; t < nk; ++t) {
-    const int cur = t & 1;
-#if W4_RING5
-    const bool more_a = t + 2 < nk;
-    i32x4 aX;
+    for (int t = 0; t < total; ++t) {
+      advance();  // the DMA cursor to stream tile t + 2
+      const bool more = jd < n_items;
+      i32x4 sX, sW;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) aX[e] = __builtin_amdgcn_readfirstlane(more_a ? srdX[e] : nullX[e]);
-#endif
+      for (int e = 0; e < 4; ++e)
+        sX[e] = __builtin_amdgcn_readfirstlane(more ? dX[e] : nullX[e]),
+        sW[e] = __builtin_amdgcn_readfirstlane(more ? dW[e] : nullW[e]);
 #pragma clang loop unroll(full)
-    for (int idx = 0; idx < SLOTS; ++idx) {  // phase A
-      mf(idx, x0, w0);
+      for (int idx = 0; idx < SLOTS; ++idx) {  // phase A
+        mf(idx, x0, w0);
 #if W4_RING5  // X(t+2) into the slot W(t-1) left (free since the barrier of tile t-1)
-      if (idx >= Sch::DA0 && (idx - Sch::DA0) % Sch::DAS == 0 && (idx - Sch::DA0) / Sch::DAS < 8)
-        dma(t + 2, (idx - Sch::DA0) / Sch::DAS, aX, aX);
+        if (idx >= Sch::DA0 && (idx - Sch::DA0) % Sch::DAS == 0 && (idx - Sch::DA0) / Sch::DAS < 8)
+          dma(t + 2, ktd, (idx - Sch::DA0) / Sch::DAS, sX, sX);
 #endif
 #ifdef W4_ABL_SPREAD  // timing ablation (racy): pieces 0..7 of tile t+2 issued in phase A
-      if (idx % (SLOTS / 8) == 2) dma(t + 2, idx / (SLOTS / 8), srdX, srdW);
+        if (idx % (SLOTS / 8) == 2) dma(t + 2, ktd, idx / (SLOTS / 8), sX, sW);
 #endif
 #ifndef W4_ABL_NOREAD
-      if (idx >= Sch::RA0 && (idx - Sch::RA0) % Sch::RAS == 0 && (idx - Sch::RA0) / Sch::RAS < 16)
-        read_frag(t, 1, (idx - Sch::RA0) / Sch::RAS, x1, w1);
+        if (idx >= Sch::RA0 && (idx - Sch::RA0) % Sch::RAS == 0 && (idx - Sch::RA0) / Sch::RAS < 16)
+          read_frag(t, 1, (idx - Sch::RA0) / Sch::RAS, x1, w1);
 #endif
-    }
+      }
 #ifdef W4_STAMPS
-    const uint64_t t_a = __builtin_amdgcn_s_memtime();
+      const uint64_t t_a = __builtin_amdgcn_s_memtime();
 #endif
 #if W4_RING5  // tile t+1 landed; X(t+2)'s 8 pieces of this phase may stay in flight
-    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #else
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #endif
 #ifdef W4_STAMPS
-    const uint64_t t_w = __builtin_amdgcn_s_memtime();
-    cyc_a += t_a - t_end, cyc_w += t_w - t_a;
+      const uint64_t t_w = __builtin_amdgcn_s_memtime();
+      cyc_a += t_a - t_end, cyc_w += t_w - t_a;
 #endif
-    phase_b(t, cur, sch);
-#ifdef W4_STAMPS
-    t_end = __builtin_amdgcn_s_memtime();
-    cyc_b += t_end - t_w;
+#if W4_RES_PF
+      if constexpr (EPI == EPI_RESIDUAL) {
+        // residual tile -> L2 over the item's last W4_RES_PF K-tiles (one dword per 128-B line,
+        // 4 lines per lane): the epilogue's reads then leave its HBM burst, which the stores
+        // of all 256 CUs saturate.  The sink VGPR stays live through the loop; its previous
+        // load is older than the 8 pieces the barrier's vmcnt(8) leaves, so it has landed.
+        asm volatile("" : : "v"(pf_sink));
+        const int r = ktc - (nk - W4_RES_PF);
+        if (split_k == 1 && r >= 0 && r % (W4_RES_PF / 4) == 0) {
+          const int line = (r / (W4_RES_PF / 4)) * 256 + tid;
+          const int row = min(gc.m0 + (line >> 2), M - 1), col = min(gc.n0 + (line & 3) * 64, N - 2);
+          const bf16_t* pf = residual + static_cast<size_t>(row) * ldc + col;
+          asm volatile("global_load_dword %0, %1, off" : "=v"(pf_sink) : "v"(pf) : "memory");
+        }
+      }
 #endif
-  }
+      phase_b(t, ktd, sX, sW, sch);
 #ifdef W4_STAMPS
-  if (lane == 0 && blockIdx.x < 4096) {
-    uint64_t* st = w4_stamps + (static_cast<size_t>(blockIdx.x) * 4 + wave) * 4;
-    st[0] = cyc_a, st[1] = cyc_w, st[2] = cyc_b, st[3] = nk;
-  }
+      t_end = __builtin_amdgcn_s_memtime();
+      cyc_b += t_end - t_w;
+#endif
+      if (split_k == 1 && ++ktc == nk) {
+        // item done: its epilogue runs while the next item's first two K-tiles land.  The last
+        // MFMAs' results are read by VALU / stores: cover the MFMA D -> read hazard first.
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+        epilogue(gc, [&](int i, int j) { return read_acc(acc[i][j]); });
+        // a counter wait hipcc sees: none of its epilogue loads is left pending across the back
+        // edge (it would otherwise wait for them, i.e. drain everything, at the top of the next
+        // K-tile).  The next item's pieces have had the whole epilogue to land.
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (expcnt / lgkmcnt unconstrained)
+        zero_acc();
+        ktc = 0;
+        if (++jc < n_items) gc = geo(jc);
+#ifdef W4_STAMPS
+        const uint64_t t_e = __builtin_amdgcn_s_memtime();
+        cyc_e += t_e - t_end;
+        t_end = t_e;
+#endif
+      }
+    }
+#ifdef W4_STAMPS
+    if (lane == 0 && blockIdx.x < 4096) {
+      uint64_t* st = w4_stamps + (static_cast<size_t>(blockIdx.x) * 4 + wave) * 8;
+      st[0] = cyc_a, st[1] = cyc_w, st[2] = cyc_b, st[3] = total;
+      st[4] = cyc_e, st[5] = __builtin_amdgcn_s_memtime() - t_start, st[6] = n_items, st[7] = 0;
+    }
 #endif
   };
   if constexpr (F8) {
@@ -440,83 +669,18 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     run(SchedMain{});
 #endif
   }
+  // every piece (the zero-range ones past the end included) has landed before the wave ends
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  // the last MFMAs' results are read by VALU / stores below: cover the MFMA D -> read hazard
+  if (split_k == 1) return;  // (the epilogues ran in the stream)
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
 
-  // ---- epilogue.  The tile is seen as [n-group][m-block] quads of 4 consecutive output columns
-  // (n) of one row (m) per lane: q = quad(i, j) with i over 32 n-groups, j over NB m-blocks.
-  //   16x16x32: block (nb, mb) lane: D[n = 16 nb + 4 fq + e][m = 16 mb + fr];  i = nb
-  //   32x32x16: block (nb, mb) lane: D[n = 32 nb + 8 g + 4 (lane >> 5) + e][m = 32 mb + (lane & 31)],
-  //             registers 4 g + e;  i = 4 nb + g (g = 0..3)
-  // value(nb, mb) returns the block's registers (accumulators, or the split-K slab sum).
-  auto epilogue = [&](auto value) {
-    constexpr int MB = L32 ? 32 : 16;
-    const int ml = L32 ? (lane & 31) : fr;
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const int m = m0 + wm * 128 + j * MB + ml;
-      if (m >= M) continue;
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) {
-        const auto blk = value(nb, j);
-        constexpr int NG = L32 ? 4 : 1;  // quads per block
-        if constexpr (EPI == EPI_SILU_MUL) {
-          // 16-row blocks of the tile alternate gate / up of the same 16 features:
-          //   16x16x32: block pairs (nb, nb+1);  32x32x16: quads g and g + 2 of one block
-          if constexpr (M32) {
-#pragma unroll
-            for (int g = 0; g < 2; ++g) {
-              const int feat = (n0 >> 1) + wn * 64 + nb * 16 + 8 * g + 4 * (lane >> 5);
-              *reinterpret_cast<u16x4*>(C + static_cast<size_t>(m) * ldc + feat) =
-                  pack4(silu(blk[4 * g]) * blk[4 * g + 8], silu(blk[4 * g + 1]) * blk[4 * g + 9],
-                        silu(blk[4 * g + 2]) * blk[4 * g + 10], silu(blk[4 * g + 3]) * blk[4 * g + 11]);
-            }
-          } else if (nb % 2 == 0) {
-            const auto u = value(nb + 1, j);
-            const int feat = (n0 >> 1) + wn * 64 + (nb >> 1) * 16 + 4 * fq;
-            *reinterpret_cast<u16x4*>(C + static_cast<size_t>(m) * ldc + feat) =
-                pack4(silu(blk[0]) * u[0], silu(blk[1]) * u[1], silu(blk[2]) * u[2], silu(blk[3]) * u[3]);
-          }
-        } else {
-#pragma unroll
-          for (int g = 0; g < NG; ++g) {
-            const int n = n0 + wn * 128 + (L32 ? nb * 32 + 8 * g + 4 * (lane >> 5) : nb * 16 + 4 * fq);
-            if (n >= N) continue;
-            float v[4] = {blk[4 * g], blk[4 * g + 1], blk[4 * g + 2], blk[4 * g + 3]};
-            if constexpr (F8) {  // dequantise: row scale x column scales
-              const float xs = x_scale[m];
-              const f32x4 wsc = *reinterpret_cast<const f32x4*>(w_scale + n);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] *= xs * wsc[e];
-            }
-            if (bias != nullptr) {
-              const u16x4 b = *reinterpret_cast<const u16x4*>(bias + n);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] += bf2f(b[e]);
-            }
-            if constexpr (EPI == EPI_RESIDUAL) {
-              const u16x4 rr = *reinterpret_cast<const u16x4*>(residual + static_cast<size_t>(m) * ldc + n);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] += bf2f(rr[e]);
-            }
-            *reinterpret_cast<u16x4*>(C + static_cast<size_t>(m) * ldc + n) = pack4(v[0], v[1], v[2], v[3]);
-          }
-        }
-      }
-    }
-  };
-
-  if (split_k == 1) {
-    epilogue([&](int i, int j) { return acc[i][j]; });
-    return;
-  }
-  // ---- split-K: every split stores its fp32 tile write-through (sc1); the last arriver sums
-  // all the slabs (its own included) straight into the epilogue -- the accumulators die at
-  // the store, so the reduction needs no second register copy of the tile.  Slab layout: per
-  // (wave, block, 16-B quarter) 256 floats, lane-major (any layout both sides agree on).
+  // ---- split-K (one item per workgroup): every split stores its fp32 tile write-through (sc1);
+  // the last arriver sums all the slabs (its own included) straight into the epilogue -- the
+  // accumulators die at the store, so the reduction needs no second register copy of the tile.
+  // Slab layout: per (wave, block, 16-B quarter) 256 floats, lane-major (any layout both sides
+  // agree on).
   constexpr int QPB = L32 ? 4 : 1;  // 16-B quarters per block per lane
-  float* slab = ws + static_cast<size_t>(tile) * split_k * (BM * BN);
+  float* slab = ws + static_cast<size_t>(gc.tile) * split_k * (BM * BN);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, split_k * BM * BN * 4, 0x00020000);
   __syncthreads();  // every wave is past its last ds_read: smem is reusable as the flag slot
   int* flag = reinterpret_cast<int*>(smem);
@@ -530,21 +694,21 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 #pragma unroll
       for (int qq = 0; qq < QPB; ++qq) {
         const f32x4 part = {acc[i][j][4 * qq], acc[i][j][4 * qq + 1], acc[i][j][4 * qq + 2], acc[i][j][4 * qq + 3]};
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, part), rs, slab_off(split, i, j, qq), 0,
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, part), rs, slab_off(gc.split, i, j, qq), 0,
                                                16 /*sc1*/);
       }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    const int prev = __hip_atomic_fetch_add(&counters[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int prev = __hip_atomic_fetch_add(&counters[gc.tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = prev == split_k - 1;
-    if (last) __hip_atomic_store(&counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (last) __hip_atomic_store(&counters[gc.tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     flag[0] = last;
   }
   __syncthreads();
   if (!flag[0]) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  epilogue([&](int i, int j) {
+  epilogue(gc, [&](int i, int j) {
     std::remove_reference_t<decltype(acc[0][0])> sum = 0.f;
     for (int sp = 0; sp < split_k; ++sp)
 #pragma unroll
@@ -558,13 +722,26 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   });
 }
 
+// compute units of the current device (one resident workgroup each: 160 KiB of LDS)
+int w4_cus() {
+  static int cus[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus[dev] = 256;
+  return cus[dev] > 0 ? cus[dev] : 256;
+}
+
 template <int EPI, bool F8 = false>
 int launch_w4(const void* x, const void* w, const void* bias, const void* res, void* c, float* ws, int* cnt, int M,
               int N, int K, int inter, int split_k, hipStream_t stream, const float* xs = nullptr,
               const float* wsc = nullptr) {
   const int m_tiles = (M + BM - 1) / BM, n_tiles = (N + BN - 1) / BN;
   const int ldc = EPI == EPI_SILU_MUL ? inter : N;
-  hipLaunchKernelGGL((gemm_w4_kernel<EPI, !F8 && W4_MFMA32 != 0, F8>), dim3(m_tiles * n_tiles * split_k), dim3(256),
+  const int nwg = m_tiles * n_tiles * split_k;
+  // persistent: one workgroup per CU streams its items (split_k == 1 only)
+  const int grid = W4_PERSIST && split_k == 1 ? std::min(nwg, w4_cus()) : nwg;
+  hipLaunchKernelGGL((gemm_w4_kernel<EPI, !F8 && W4_MFMA32 != 0, F8>), dim3(grid), dim3(256),
                      0, stream, x, w, static_cast<const bf16_t*>(bias), static_cast<const bf16_t*>(res),
                      static_cast<bf16_t*>(c), ws, cnt, M, N, K, ldc, inter, m_tiles, n_tiles, split_k, xs, wsc);
   return BCG_CHECK_LAUNCH();

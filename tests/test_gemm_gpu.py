@@ -131,6 +131,30 @@ def test_gemm_pp_edges(hip, M, N, K, epi, cfg):
         _close(got, want)
 
 
+@pytest.mark.parametrize("M,N,K", [(4096 + 77, 4112, 1024), (16384, 1280, 256), (9000, 2560, 64), (300, 74752, 128)])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+def test_gemm_w4_persistent_many_items(hip, M, N, K, epi):
+    """cfg 11's persistent launch: more tiles than CUs, so a workgroup streams several items
+    (epilogue of one while the next one's first K-tiles land), partial last tiles in M and N,
+    1-16 K-tiles per item, repeated launches."""
+    torch.manual_seed(M + N + K + epi)
+    if epi == 1:
+        N -= N % 256  # (the fused SiLU needs inter % 128 == 0)
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
+    ref = _ref(x, w)
+    for _ in range(2):
+        if epi == 2:
+            r = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+            want = r.float() + ref
+            _close(hip.gemm_nt(x, w, 11, 2, residual=r, out=r), want)
+        elif epi == 1:
+            I = N // 2
+            _close(hip.gemm_nt(x, w, 11, 1), torch.nn.functional.silu(ref[:, :I]) * ref[:, I:])
+        else:
+            _close(hip.gemm_nt(x, w, 11, 0), ref)
+
+
 @pytest.mark.parametrize("cfg", [10, 11])
 def test_gemm_pp_prefill_chunk_silu(hip, cfg):
     """A prefill-sized gate_up chunk through the 256x256 kernels with the fused SiLU*mul."""
