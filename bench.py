@@ -416,6 +416,11 @@ def main(argv=None):
     cpu0 = time.process_time()  # this rank's host CPU (all threads) over the timed region
     a0 = accepted()
     per_window, steps_done, last = [], 0, a0
+
+    def eng_tokens():  # uncached prompt + generated tokens so far (the engine's live counters)
+        return eng.get("prompt_tokens", 0) - eng.get("cached_tokens", 0) + eng.get("generated_tokens", 0)
+
+    tok_windows, tok_last = [], eng_tokens()
     # the deadline is agreed on by every rank (the slowest start wins)
     budget = torch.tensor([args.deadline_s - (t_start - t_origin)], dtype=torch.float64)
     if world > 1:
@@ -428,6 +433,9 @@ def main(argv=None):
         now = accepted()
         per_window.append(now - last)
         last = now
+        t_now = eng_tokens()
+        tok_windows.append(t_now - tok_last)
+        tok_last = t_now
         steps_done += 1
     decisions = last - a0
     host_cpu_s = time.process_time() - cpu0
@@ -503,6 +511,9 @@ def main(argv=None):
                        "fill_s": round(fill_s, 1), "fill_max_s": args.fill_max_s,
                        "fill_capped": fill_s >= args.fill_max_s - 0.5,
                        "tokens_per_s": round(tokens_per_s, 1), "window_stats_rank0": stats,
+                       # the same spread for the engine's token count per window: the smooth
+                       # series A/B comparisons should use
+                       "token_window_stats_rank0": window_stats(tok_windows, args.window_s),
                        "host": {"cpu_s_all_ranks": round(host_cpu_s, 1),
                                 "cpu_s_per_decision": (round(host_cpu_s / total_decisions, 4)
                                                        if total_decisions else None),

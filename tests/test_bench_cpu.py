@@ -83,7 +83,7 @@ def test_bench_reports_resolution_fields():
     out = _run(["--steps", "4", "--warmup", "1", "--max-rounds", "7"])
     d = out["detail"]
     assert out["config"]["max_rounds"] == 7
-    assert {"tokens_per_s", "window_stats_rank0", "fill_max_s", "fill_capped"} <= set(d)
+    assert {"tokens_per_s", "window_stats_rank0", "token_window_stats_rank0", "fill_max_s", "fill_capped"} <= set(d)
     assert d["window_stats_rank0"]["n"] == 4
     assert "protocol" in d["age_mix"]
 
