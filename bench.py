@@ -546,7 +546,13 @@ def main(argv=None):
     llm.shutdown()
     if world > 1:
         barrier()
-        dist.destroy_process_group()
+        from byzantine_consensus_llm_agents_amd.parallel import groups
+        groups.destroy()  # custom all-reduce buffers unmapped while every peer is still alive
+        # skip interpreter finalization: a daemon game thread unwound inside native code
+        # there (pthread_exit through a noexcept frame) aborts the rank after its result is out
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 if __name__ == "__main__":
