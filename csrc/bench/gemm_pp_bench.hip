@@ -19,6 +19,14 @@ extern "C" int bcg_gemm_w4_stamps(void* host, int n);
 #endif
 extern "C" int GEMM_FN(int epi, const void* x, const void* w, const void* bias, const void* residual, void* c,
                        void* ws, void* counters, int M, int N, int K, int inter, int split_k, hipStream_t stream);
+#ifdef BENCH_FP8  // e4m3fn operands through bcg_gemm_w4_fp8 (EPI 0 / 2)
+extern "C" int bcg_gemm_w4_fp8(int epi, const void* xq, const void* wq, const float* x_scale, const float* w_scale,
+                               const void* bias, const void* residual, void* c, void* ws, void* counters, int M, int N,
+                               int K, int split_k, hipStream_t stream);
+constexpr size_t ESZ = 1;
+#else
+constexpr size_t ESZ = 2;
+#endif
 
 __global__ void fill_bf16(uint16_t* p, size_t n, uint32_t seed, float scale) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -30,6 +38,17 @@ __global__ void fill_bf16(uint16_t* p, size_t n, uint32_t seed, float scale) {
     h ^= h >> 16;
     const float v = ((h & 0xffffff) / 16777216.0f * 2.f - 1.f) * scale;
     p[i] = (uint16_t)(__float_as_uint(v) >> 16);
+  }
+}
+
+// e4m3fn bytes with the exponent field below 1111 (never NaN): (hash & 0x77)
+__global__ void fill_fp8(uint8_t* p, size_t n, uint32_t seed) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    p[i] = (uint8_t)((h & 0x77) | ((h >> 8) & 0x80));
   }
 }
 
@@ -49,18 +68,31 @@ int main(int argc, char** argv) {
   }
   const int M = atoi(argv[1]), N = atoi(argv[2]), K = atoi(argv[3]), epi = atoi(argv[4]), split = atoi(argv[5]);
   const int iters = argc > 6 ? atoi(argv[6]) : 20;
-  const size_t wbytes = (size_t)N * K * 2;
+  const size_t wbytes = (size_t)N * K * ESZ;
   const int copies = (int)std::max<size_t>(2, std::min<size_t>(8, ((size_t)1 << 30) / wbytes + 1));
   uint16_t *x, *r, *c;
   std::vector<uint16_t*> w(copies);
-  CK(hipMalloc(&x, (size_t)M * K * 2));
+  CK(hipMalloc(&x, (size_t)M * K * ESZ));
   CK(hipMalloc(&r, (size_t)M * N * 2));
   CK(hipMalloc(&c, (size_t)M * N * 2));
-  hipLaunchKernelGGL(fill_bf16, dim3(1024), dim3(256), 0, 0, x, (size_t)M * K, 1u, 1.f);
   hipLaunchKernelGGL(fill_bf16, dim3(1024), dim3(256), 0, 0, r, (size_t)M * N, 2u, 1.f);
+#ifdef BENCH_FP8
+  float *xs, *wsc;
+  CK(hipMalloc(&xs, (size_t)M * 4));
+  CK(hipMalloc(&wsc, (size_t)N * 4));
+  CK(hipMemset(xs, 0, (size_t)M * 4));
+  CK(hipMemset(wsc, 0, (size_t)N * 4));
+  hipLaunchKernelGGL(fill_fp8, dim3(1024), dim3(256), 0, 0, (uint8_t*)x, (size_t)M * K, 1u);
+#else
+  hipLaunchKernelGGL(fill_bf16, dim3(1024), dim3(256), 0, 0, x, (size_t)M * K, 1u, 1.f);
+#endif
   for (int i = 0; i < copies; ++i) {
     CK(hipMalloc(&w[i], wbytes));
+#ifdef BENCH_FP8
+    hipLaunchKernelGGL(fill_fp8, dim3(1024), dim3(256), 0, 0, (uint8_t*)w[i], (size_t)N * K, 3u + i);
+#else
     hipLaunchKernelGGL(fill_bf16, dim3(1024), dim3(256), 0, 0, w[i], (size_t)N * K, 3u + i, 0.05f);
+#endif
   }
   const int tiles = (M + 255) / 256 * ((N + 255) / 256);
   float* ws = nullptr;
@@ -73,7 +105,11 @@ int main(int argc, char** argv) {
   auto run = [&](int i) {
     const void* res = epi == 2 ? r : nullptr;
     void* out = epi == 2 ? (void*)r : (void*)c;
+#ifdef BENCH_FP8
+    return bcg_gemm_w4_fp8(epi, x, w[i % copies], xs, wsc, nullptr, res, out, ws, cnt, M, N, K, split, 0);
+#else
     return GEMM_FN(epi, x, w[i % copies], nullptr, res, out, ws, cnt, M, N, K, N / 2, split, 0);
+#endif
   };
   for (int i = 0; i < 5; ++i)
     if (run(i)) {

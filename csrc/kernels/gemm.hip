@@ -51,7 +51,9 @@ typedef bf16x8 bf16x8s;  // MFMA operand (8 x bf16, 16 B)
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
-__device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
+// g * sigmoid(g) with the hardware reciprocal (1 ulp; a true division expands to ~10
+// instructions with mode switches per element in the epilogue)
+__device__ __forceinline__ float silu(float g) { return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
 
 // Stage `rows` rows x 64 K of a row-major [*, K] bf16 matrix into a linear LDS image
 // (row r at byte r*128, swizzled chunks).  Every wave issues rows/32 glds of 8 rows each.

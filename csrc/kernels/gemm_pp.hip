@@ -96,7 +96,9 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
-__device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
+// g * sigmoid(g) with the hardware reciprocal (1 ulp; a true division expands to ~10
+// instructions with mode switches per element in the epilogue)
+__device__ __forceinline__ float silu(float g) { return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
 
 __device__ __forceinline__ void sbar() {
 #ifndef PP_NO_SCHED_BARRIER

@@ -41,6 +41,9 @@
 
 #include "common.h"
 
+#ifndef W4_GROUP_M_F8
+#define W4_GROUP_M_F8 4  // (fp8: 4 measured +2-15 % over 8 on Mistral-22B prefill shapes, profiles/r4_gemm_w4)
+#endif
 #ifndef W4_GROUP_M
 #define W4_GROUP_M 8  // m-tiles per tile-order group (L2 reuse of both operands)
 #endif
@@ -116,6 +119,7 @@ constexpr int A_BYTES = BM * 128, STAGE = A_BYTES + BN * 128;  // 64 KiB
 enum Epilogue { EPI_STORE = 0, EPI_SILU_MUL = 1, EPI_RESIDUAL = 2 };
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 static_assert(W4_RA0 + 15 * W4_RAS < W4_SLOTS && W4_DB0 + (W4_NPB - 1) * W4_DBS < W4_SLOTS &&
@@ -123,7 +127,9 @@ static_assert(W4_RA0 + 15 * W4_RAS < W4_SLOTS && W4_DB0 + (W4_NPB - 1) * W4_DBS 
               "each stream fits its phase");
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
+// g * sigmoid(g) with the hardware reciprocal (1 ulp; a true division expands to ~10
+// instructions with mode switches per element in the epilogue)
+__device__ __forceinline__ float silu(float g) { return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
 
 __device__ __forceinline__ u16x4 pack4(float a, float b, float c, float d) {
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -219,9 +225,10 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     Geo g;
     g.split = r_id % split_k;
     g.tile = r_id / split_k;
-    const int grp = g.tile / (W4_GROUP_M * n_tiles), in_grp = g.tile % (W4_GROUP_M * n_tiles);
-    const int gm = min(m_tiles - grp * W4_GROUP_M, W4_GROUP_M);
-    g.m0 = (grp * W4_GROUP_M + in_grp % gm) * BM;
+    constexpr int GM = F8 ? W4_GROUP_M_F8 : W4_GROUP_M;
+    const int grp = g.tile / (GM * n_tiles), in_grp = g.tile % (GM * n_tiles);
+    const int gm = min(m_tiles - grp * GM, GM);
+    g.m0 = (grp * GM + in_grp % gm) * BM;
     g.n0 = (in_grp / gm) * BN;
     return g;
   };
@@ -372,6 +379,12 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       if (++jd < n_items) item_srd(geo(jd), dX, dW);
     }
   };
+#ifdef W4_DESYNC  // timing experiment: odd workgroups start nk x W4_DESYNC cycles late (epilogues staggered)
+  if (blockIdx.x & 1) {
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - t0 < static_cast<uint64_t>(nk) * W4_DESYNC) __builtin_amdgcn_s_sleep(10);
+  }
+#endif
   // ---- prologue: stream tiles 0 and 1 in flight, tile 0 landed, k-step 0 of tile 0 in registers ----
 #pragma unroll
   for (int q = 0; q < 16; ++q) dma(0, 0, q, dX, dW);
@@ -410,6 +423,131 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       *reinterpret_cast<u16x4*>(p) = v;
 #endif
     };
+    if constexpr (!L32) {
+      // 16x16 layout, buffer-addressed, 16-B accesses.  A store costs per cache line it touches
+      // (stamps: ~300 cycles a 16-row x 8-B store, the same for 16 rows x 16 B), so two
+      // neighbouring quads (4 columns of blocks 2p and 2p+1) are turned into 8 contiguous
+      // columns per lane by one v_permlane16_swap per value: afterwards lane row fq holds
+      // block 2p + (fq & 1), columns 8 (fq >> 1) .. +7 -- half the stores and loads.
+      // Offsets are bytes from the item's output corner (C + m0 ldc + its first column): rows
+      // past M fall outside the descriptor's range (stores dropped, loads 0), a column past N
+      // gets an offset past every range, m-block j's rows ride in the SGPR offset -- no
+      // per-quad branch, no 64-bit address math.
+      constexpr bool SILU = EPI == EPI_SILU_MUL;
+      constexpr int NP = SILU ? NB / 4 : NB / 2;  // 8-column groups per m-block per lane
+      constexpr int JG = 2;                       // m-blocks per residual batch
+      const uint32_t ldb = static_cast<uint32_t>(ldc) * 2;
+      const int c0 = SILU ? (n0 >> 1) : n0;
+      const uint32_t range = static_cast<uint32_t>(M - m0) * ldb;
+      const auto rc = __builtin_amdgcn_make_buffer_rsrc(C + static_cast<size_t>(m0) * ldc + c0, 0, range, 0x00020000);
+      const uint32_t rowv = static_cast<uint32_t>(wm * 128 + fr) * ldb;
+      uint32_t colv[NP];
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const int cl = (SILU ? wn * 64 : wn * 128) + (2 * p + (fq & 1)) * 16 + (fq >> 1) * 8;
+        colv[p] = SILU || n0 + cl < N ? static_cast<uint32_t>(cl) * 2 : 0x80000000u;
+      }
+      // lane-pair swap: a = 4 columns of the even quad, b = of the odd one -> o = 8 columns
+      auto swap8 = [](const float (&a)[4], const float (&b)[4], float (&o)[8]) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[e]), __float_as_uint(b[e]), false, false);
+          o[e] = __uint_as_float(r[0]);
+          o[4 + e] = __uint_as_float(r[1]);
+        }
+      };
+      auto store8 = [&](int j, int p, const float (&o)[8]) {
+        const u32x2 lo = __builtin_bit_cast(u32x2, pack4(o[0], o[1], o[2], o[3]));
+        const u32x2 hi = __builtin_bit_cast(u32x2, pack4(o[4], o[5], o[6], o[7]));
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo[0], lo[1], hi[0], hi[1]}, rc, rowv + colv[p],
+                                               static_cast<uint32_t>(j * MB) * ldb, 0);
+      };
+      if constexpr (SILU) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+#pragma unroll
+          for (int p = 0; p < NP; ++p) {
+            // 16-row blocks of the tile alternate gate / up of the same 16 features: output quad
+            // q = blocks 2q (gate) and 2q + 1 (up); the pair p = quads 2p, 2p + 1
+            float h[2][4];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+              const auto g = value(4 * p + 2 * k, j), u = value(4 * p + 2 * k + 1, j);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) h[k][e] = silu(g[e]) * u[e];
+            }
+            float o[8];
+            swap8(h[0], h[1], o);
+            store8(j, p, o);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+        const auto rr_rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<bf16_t*>(EPI == EPI_RESIDUAL ? residual + static_cast<size_t>(m0) * ldc + n0 : C), 0,
+            EPI == EPI_RESIDUAL ? range : 0u, 0x00020000);
+        // residual groups (8 bf16 per lane): batches of JG m-blocks, the next batch loaded
+        // before this one is used
+        u32x4 rq[2][JG][NP];
+        auto load_rq = [&](int bf, int j0) {
+          if constexpr (EPI == EPI_RESIDUAL) {
+#pragma unroll
+            for (int jj = 0; jj < JG; ++jj)
+#pragma unroll
+              for (int p = 0; p < NP; ++p)
+                rq[bf][jj][p] = __builtin_amdgcn_raw_buffer_load_b128(rr_rs, rowv + colv[p],
+                                                                      static_cast<uint32_t>((j0 + jj) * MB) * ldb, 0);
+          }
+        };
+        // one body per bias case (a uniform branch here, not one per quad); the bias groups
+        // are widened to fp32 once per item
+        auto body = [&](auto has_bias) {
+          constexpr bool HB = decltype(has_bias)::value;
+          float bq[HB ? NP : 1][8];
+          if constexpr (HB) {
+            const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(bias + n0), 0,
+                                                              static_cast<uint32_t>(N - n0) * 2, 0x00020000);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+              const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rb, colv[p], 0, 0);
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                bq[p][2 * e] = __uint_as_float(b[e] << 16), bq[p][2 * e + 1] = __uint_as_float(b[e] & 0xffff0000u);
+            }
+          }
+          load_rq(0, 0);
+#pragma unroll
+          for (int j0 = 0; j0 < NB; j0 += JG) {
+            const int bf = (j0 / JG) & 1;
+            if (j0 + JG < NB) load_rq(bf ^ 1, j0 + JG);
+#pragma unroll
+            for (int jj = 0; jj < JG; ++jj)
+#pragma unroll
+              for (int p = 0; p < NP; ++p) {
+                const auto a = value(2 * p, j0 + jj), b = value(2 * p + 1, j0 + jj);
+                const float fa[4] = {a[0], a[1], a[2], a[3]}, fb[4] = {b[0], b[1], b[2], b[3]};
+                float o[8];
+                swap8(fa, fb, o);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                  if constexpr (HB) o[e] += bq[p][e];
+                  if constexpr (EPI == EPI_RESIDUAL) {
+                    const uint32_t w = rq[bf][jj][p][e >> 1];
+                    o[e] += __uint_as_float((e & 1) ? (w & 0xffff0000u) : (w << 16));
+                  }
+                }
+                store8(j0 + jj, p, o);
+              }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        };
+        if (bias != nullptr)
+          body(std::true_type{});
+        else
+          body(std::false_type{});
+      }
+      return;
+    }
     if constexpr (EPI == EPI_SILU_MUL) {
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
@@ -465,40 +603,110 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
                                                              ncl(col(q)));
         }
       };
-      // (fp8: its scale loads need those registers -- residual quads are loaded where used)
-      if (!F8) load_batch(0, 0);
+      if constexpr (F8) {
+        // fp8 (32x32 blocks): lane (r = lane & 31, h = lane >> 5) holds, per block and quad g,
+        // columns 8 g + 4 h .. +3 of row r.  Scales go on per quad, then one v_permlane32_swap
+        // per value turns quads g, g + 1 (g = 0, 2) into 8 contiguous columns per lane (h = 0:
+        // 8 g .., h = 1: 8 (g + 1) ..): 16-B stores and loads, half the instructions (a store
+        // costs per row it touches).  Buffer addressing as the 16x16 path; the residual and bias
+        // descriptors have a zero range when unused (loads return 0).
+        const int h = ln >> 5;
+        const uint32_t ldb = static_cast<uint32_t>(ldc) * 2;
+        const uint32_t range = static_cast<uint32_t>(M - m0) * ldb;
+        const auto rc = __builtin_amdgcn_make_buffer_rsrc(C + static_cast<size_t>(m0) * ldc + n0, 0, range, 0x00020000);
+        const auto rres = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<bf16_t*>(EPI == EPI_RESIDUAL ? residual + static_cast<size_t>(m0) * ldc + n0 : C), 0,
+            EPI == EPI_RESIDUAL ? range : 0u, 0x00020000);
+        const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(bias != nullptr ? bias + n0 : C), 0,
+                                                          bias != nullptr ? static_cast<uint32_t>(N - n0) * 2 : 0u,
+                                                          0x00020000);
+        const uint32_t rowv = static_cast<uint32_t>(wm * 128 + ml) * ldb;
+        float xsr[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) xsr[j] = x_scale[mcl(row(j))];
+        auto widen8 = [](const u32x4& w, float (&o)[8]) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            o[2 * e] = __uint_as_float(w[e] << 16), o[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+        };
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          uint32_t colv[2];
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp) {
+            const int cl = wn * 128 + nb * 32 + 8 * (2 * pp + h);
+            colv[pp] = n0 + cl < N ? static_cast<uint32_t>(cl) * 2 : 0x80000000u;
+          }
+          f32x4 wsq[NG];
+#pragma unroll
+          for (int g = 0; g < NG; ++g) wsq[g] = *reinterpret_cast<const f32x4*>(w_scale + ncl(col(nb * NG + g)));
+          u32x4 rq[NB][2], bq[2];
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp) {
+            bq[pp] = __builtin_amdgcn_raw_buffer_load_b128(rb, colv[pp], 0, 0);
+            if constexpr (EPI == EPI_RESIDUAL) {
+#pragma unroll
+              for (int j = 0; j < NB; ++j)
+                rq[j][pp] = __builtin_amdgcn_raw_buffer_load_b128(rres, rowv + colv[pp],
+                                                                  static_cast<uint32_t>(j * MB) * ldb, 0);
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < NB; ++j) {
+            const auto blk = value(nb, j);
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp) {
+              const int g = 2 * pp;
+              float o[8], add[8];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const auto r = __builtin_amdgcn_permlane32_swap(
+                    __float_as_uint(blk[4 * g + e] * (xsr[j] * wsq[g][e])),
+                    __float_as_uint(blk[4 * (g + 1) + e] * (xsr[j] * wsq[g + 1][e])), false, false);
+                o[e] = __uint_as_float(r[0]);
+                o[4 + e] = __uint_as_float(r[1]);
+              }
+              widen8(bq[pp], add);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) o[e] += add[e];
+              if constexpr (EPI == EPI_RESIDUAL) {
+                widen8(rq[j][pp], add);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[e] += add[e];
+              }
+              const u32x2 lo = __builtin_bit_cast(u32x2, pack4(o[0], o[1], o[2], o[3]));
+              const u32x2 hi = __builtin_bit_cast(u32x2, pack4(o[4], o[5], o[6], o[7]));
+              __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo[0], lo[1], hi[0], hi[1]}, rc, rowv + colv[pp],
+                                                     static_cast<uint32_t>(j * MB) * ldb, 0);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        return;
+      }
+      load_batch(0, 0);
 #pragma unroll
       for (int j0 = 0; j0 < NB; j0 += JG) {
         const int bf = (j0 / JG) & 1;
-        if (!F8 && j0 + JG < NB) load_batch(bf ^ 1, j0 + JG);
+        if (j0 + JG < NB) load_batch(bf ^ 1, j0 + JG);
 #pragma unroll
         for (int jj = 0; jj < JG; ++jj) {
           const int j = j0 + jj, m = row(j);
-          if (F8 && m >= M) continue;  // (fp8: no residual batch; masked rows skip their scale loads)
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb) {
             const auto blk = value(nb, j);
 #pragma unroll
             for (int g = 0; g < NG; ++g) {
               const int q = nb * NG + g, n = col(q);
-              if (F8 && n >= N) continue;
               float v[4] = {blk[4 * g], blk[4 * g + 1], blk[4 * g + 2], blk[4 * g + 3]};
-              if constexpr (F8) {  // dequantise: row scale x column scales
-                const float xs = x_scale[m];
-                const f32x4 wsc = *reinterpret_cast<const f32x4*>(w_scale + n);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] *= xs * wsc[e];
-              }
               if (bias != nullptr) {
                 const u16x4 b = *reinterpret_cast<const u16x4*>(bias + ncl(n));
 #pragma unroll
                 for (int e = 0; e < 4; ++e) v[e] += bf2f(b[e]);
               }
               if constexpr (EPI == EPI_RESIDUAL) {
-                const u16x4 r4 =
-                    F8 ? *reinterpret_cast<const u16x4*>(residual + static_cast<size_t>(m) * ldc + n) : rr[bf][jj][q];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] += bf2f(r4[e]);
+                for (int e = 0; e < 4; ++e) v[e] += bf2f(rr[bf][jj][q][e]);
               }
               if (m < M && n < N) st4(C + static_cast<size_t>(m) * ldc + n, pack4(v[0], v[1], v[2], v[3]));
             }
