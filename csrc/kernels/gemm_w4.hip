@@ -94,6 +94,9 @@
 #define W4_ABL_PIECE0 0
 #endif
 #define W4_NPB (W4_RING5 ? 8 : W4_ABL_NPIECE)  // pieces issued in phase B
+#ifndef W4_STAGE_EPI
+#define W4_STAGE_EPI 0  // stores staged through the free ring slot, whole rows per store; measured: +-0.7 %, off
+#endif
 #ifndef W4_RES_PF
 #define W4_RES_PF 0  // residual tile -> L2 over an item's last N K-tiles (N % 4 == 0); measured: no gain
 #endif
@@ -405,7 +408,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   //   32x32x16: block (nb, mb) lane: D[n = 32 nb + 8 g + 4 (lane >> 5) + e][m = 32 mb + (lane & 31)],
   //             registers 4 g + e;  i = 4 nb + g (g = 0..3)
   // value(nb, mb) returns the block's registers (accumulators, or the split-K slab sum).
-  auto epilogue = [&](const Geo& geo_c, auto value) {
+  auto epilogue = [&](const Geo& geo_c, auto value, uint32_t stage = 0xffffffffu) {
     constexpr int MB = L32 ? 32 : 16;
     constexpr int NG = L32 ? 4 : 1;  // quads per block
     // the lane index re-enters here through an opaque move: the epilogue's per-lane address
@@ -435,7 +438,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       // per-quad branch, no 64-bit address math.
       constexpr bool SILU = EPI == EPI_SILU_MUL;
       constexpr int NP = SILU ? NB / 4 : NB / 2;  // 8-column groups per m-block per lane
-      constexpr int JG = 2;                       // m-blocks per residual batch
+      constexpr int JG = 1;                       // m-blocks per residual batch
       const uint32_t ldb = static_cast<uint32_t>(ldc) * 2;
       const int c0 = SILU ? (n0 >> 1) : n0;
       const uint32_t range = static_cast<uint32_t>(M - m0) * ldb;
@@ -456,11 +459,44 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
           o[4 + e] = __uint_as_float(r[1]);
         }
       };
-      auto store8 = [&](int j, int p, const float (&o)[8]) {
+      // With a staging slot (the ring slot tile t's W half left: free from the barrier after phase
+      // A(t) until phase A(t+1) refills it), the 8 columns go to LDS instead, 32 rows per pass,
+      // and come back row-major: every global store then writes 4 (SILU: 8) whole rows of the
+      // wave's 256 (128) B instead of 16 rows x 64 B.  XOR-swizzled 16-B chunks keep both the
+      // fragment-order writes and the row-order reads conflict-free.
+      constexpr int CH = SILU ? 8 : 16;  // 16-B chunks per staged row (the wave's columns)
+      const bool staged = stage != 0xffffffffu;
+      const uint32_t sbase = stage + static_cast<uint32_t>(wave) * (32 * CH * 16);
+      auto swz = [](int r) { return CH == 16 ? (r & 15) : ((r >> 1) & 7); };
+      auto pack8 = [](const float (&o)[8]) {
         const u32x2 lo = __builtin_bit_cast(u32x2, pack4(o[0], o[1], o[2], o[3]));
         const u32x2 hi = __builtin_bit_cast(u32x2, pack4(o[4], o[5], o[6], o[7]));
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo[0], lo[1], hi[0], hi[1]}, rc, rowv + colv[p],
-                                               static_cast<uint32_t>(j * MB) * ldb, 0);
+        return u32x4{lo[0], lo[1], hi[0], hi[1]};
+      };
+      auto store8 = [&](int j, int p, const float (&o)[8]) {
+        if (staged) {  // row (j & 1) * 16 + fr of the pass, chunk 4 p + 2 (fq & 1) + (fq >> 1)
+          const int r = (j & 1) * 16 + fr, c = 4 * p + 2 * (fq & 1) + (fq >> 1);
+          *reinterpret_cast<u32x4*>(smem + sbase + (r * CH + (c ^ swz(r))) * 16) = pack8(o);
+          return;
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(pack8(o), rc, rowv + colv[p], static_cast<uint32_t>(j * MB) * ldb, 0);
+      };
+      // the pass of m-blocks j0, j0 + 1 (rows 16 j0 ..): read row-major, store whole rows
+      auto flush = [&](int j0) {
+        if (!staged) return;
+        constexpr int LPR = CH;           // lanes per row
+        constexpr int RPI = 64 / LPR;     // rows per instruction
+        const int c = lane & (LPR - 1);
+        const int cl = (SILU ? wn * 64 : wn * 128) + c * 8;
+        const uint32_t cv = SILU || n0 + cl < N ? static_cast<uint32_t>(cl) * 2 : 0x80000000u;
+#pragma unroll
+        for (int i = 0; i < 32 / RPI; ++i) {
+          const int r = i * RPI + lane / LPR;
+          const u32x4 v = *reinterpret_cast<const u32x4*>(smem + sbase + (r * CH + (c ^ swz(r))) * 16);
+          __builtin_amdgcn_raw_buffer_store_b128(v, rc, static_cast<uint32_t>(wm * 128 + r) * ldb + cv,
+                                                 static_cast<uint32_t>(j0 * MB) * ldb, 0);
+          if (i & 1) __builtin_amdgcn_sched_barrier(0);  // (two rows of reads in flight, not all)
+        }
       };
       if constexpr (SILU) {
 #pragma unroll
@@ -480,6 +516,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
             swap8(h[0], h[1], o);
             store8(j, p, o);
           }
+          if (j & 1) flush(j - 1);
           __builtin_amdgcn_sched_barrier(0);
         }
       } else {
@@ -503,17 +540,12 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         // are widened to fp32 once per item
         auto body = [&](auto has_bias) {
           constexpr bool HB = decltype(has_bias)::value;
-          float bq[HB ? NP : 1][8];
+          u32x4 bq[HB ? NP : 1];  // 8 bf16 per group, widened where used
           if constexpr (HB) {
             const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(bias + n0), 0,
                                                               static_cast<uint32_t>(N - n0) * 2, 0x00020000);
 #pragma unroll
-            for (int p = 0; p < NP; ++p) {
-              const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rb, colv[p], 0, 0);
-#pragma unroll
-              for (int e = 0; e < 4; ++e)
-                bq[p][2 * e] = __uint_as_float(b[e] << 16), bq[p][2 * e + 1] = __uint_as_float(b[e] & 0xffff0000u);
-            }
+            for (int p = 0; p < NP; ++p) bq[p] = __builtin_amdgcn_raw_buffer_load_b128(rb, colv[p], 0, 0);
           }
           load_rq(0, 0);
 #pragma unroll
@@ -530,7 +562,10 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
                 swap8(fa, fb, o);
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
-                  if constexpr (HB) o[e] += bq[p][e];
+                  if constexpr (HB) {
+                    const uint32_t w = bq[p][e >> 1];
+                    o[e] += __uint_as_float((e & 1) ? (w & 0xffff0000u) : (w << 16));
+                  }
                   if constexpr (EPI == EPI_RESIDUAL) {
                     const uint32_t w = rq[bf][jj][p][e >> 1];
                     o[e] += __uint_as_float((e & 1) ? (w & 0xffff0000u) : (w << 16));
@@ -538,6 +573,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
                 }
                 store8(j0 + jj, p, o);
               }
+            if (j0 & 1) flush(j0 - 1);  // one staging pass per two m-blocks
             __builtin_amdgcn_sched_barrier(0);
           }
         };
@@ -839,7 +875,11 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         // item done: its epilogue runs while the next item's first two K-tiles land.  The last
         // MFMAs' results are read by VALU / stores: cover the MFMA D -> read hazard first.
         asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
-        epilogue(gc, [&](int i, int j) { return read_acc(acc[i][j]); });
+        epilogue(gc, [&](int i, int j) { return read_acc(acc[i][j]); }, W4_STAGE_EPI && W4_RING5 ? slot_off(t, 1) : 0xffffffffu);
+#if W4_STAGE_EPI && W4_RING5
+        // every wave's staging reads are done before phase A(t+1) loads X(t+3) into that slot
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
         // a counter wait hipcc sees: none of its epilogue loads is left pending across the back
         // edge (it would otherwise wait for them, i.e. drain everything, at the top of the next
         // K-tile).  The next item's pieces have had the whole epilogue to land.
