@@ -408,6 +408,99 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
   }
 
   // ---- epilogue: lane holds D[n = 4fq + e][m = fr] of block (nb, mb) ----
+  if constexpr (!F8) {
+    // bf16: buffer-addressed and 16-B wide, as csrc/kernels/gemm_w4.hip: one v_permlane16_swap
+    // per value turns the quads of blocks (2p, 2p+1) into 8 contiguous columns per lane (lane
+    // row fq: block 2p + (fq & 1), columns 8 (fq >> 1) ..); rows past M fall outside the
+    // descriptor's range, a column past N gets an out-of-range offset, m-block mb's rows ride in
+    // the SGPR offset.  Half the stores, no per-quad branch.
+    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+    typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+    constexpr bool SILU = EPI == EPI_SILU_MUL;
+    // the lane index re-enters through an opaque move: none of the epilogue's per-lane address
+    // math is hoisted above the K-loop (it would hold VGPRs across it)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int fr = ln & 15, fq = ln >> 4;
+    const uint32_t ldb = static_cast<uint32_t>(ldc) * 2;
+    const uint32_t range = static_cast<uint32_t>(M - m0) * ldb;
+    const auto rc = __builtin_amdgcn_make_buffer_rsrc(C + static_cast<size_t>(m0) * ldc + (SILU ? (n0 >> 1) : n0), 0,
+                                                      range, 0x00020000);
+    const uint32_t rowv = static_cast<uint32_t>(g * 128 + fr) * ldb;
+    auto swap_store = [&](int mb, uint32_t colv, const float (&a)[4], const float (&b)[4], const u32x4v& add0,
+                          const u32x4v& add1) {
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[e]), __float_as_uint(b[e]), false, false);
+        o[e] = __uint_as_float(r[0]);
+        o[4 + e] = __uint_as_float(r[1]);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t w0 = add0[e >> 1], w1 = add1[e >> 1];
+        o[e] += __uint_as_float((e & 1) ? (w0 & 0xffff0000u) : (w0 << 16)) +
+                __uint_as_float((e & 1) ? (w1 & 0xffff0000u) : (w1 << 16));
+      }
+      u16x4 lo, hi;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) lo[e] = f2bf(o[e]), hi[e] = f2bf(o[4 + e]);
+      const u32x2v l2 = __builtin_bit_cast(u32x2v, lo), h2 = __builtin_bit_cast(u32x2v, hi);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4v{l2[0], l2[1], h2[0], h2[1]}, rc, rowv + colv,
+                                             static_cast<uint32_t>(mb * 16) * ldb, 0);
+    };
+    const u32x4v zero = {0, 0, 0, 0};
+    if constexpr (SILU) {
+      const uint32_t colv = static_cast<uint32_t>(wc * 32 + (fq & 1) * 16 + (fq >> 1) * 8) * 2;
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) {
+        float h[2][4];
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh)  // (gate, up) block pairs of the same 16 features
+#pragma unroll
+          for (int e = 0; e < 4; ++e) h[nh][e] = silu(acc[2 * nh][mb][e]) * acc[2 * nh + 1][mb][e];
+        swap_store(mb, colv, h[0], h[1], zero, zero);
+      }
+    } else {
+      uint32_t colv[2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int cl = wc * 64 + (2 * p + (fq & 1)) * 16 + (fq >> 1) * 8;
+        colv[p] = n0 + cl < N ? static_cast<uint32_t>(cl) * 2 : 0x80000000u;
+      }
+      // bias / residual through zero-range descriptors when absent (loads return 0)
+      const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(bias != nullptr ? bias + n0 : C), 0,
+                                                        bias != nullptr ? static_cast<uint32_t>(N - n0) * 2 : 0u,
+                                                        0x00020000);
+      const auto rr = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<bf16_t*>(EPI == EPI_RESIDUAL ? residual + static_cast<size_t>(m0) * ldc + n0 : C), 0,
+          EPI == EPI_RESIDUAL ? range : 0u, 0x00020000);
+      u32x4v bq[2], rq[2][2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        bq[p] = __builtin_amdgcn_raw_buffer_load_b128(rb, colv[p], 0, 0);
+        rq[0][p] = EPI == EPI_RESIDUAL ? __builtin_amdgcn_raw_buffer_load_b128(rr, rowv + colv[p], 0, 0) : zero;
+      }
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) {
+        const int cur = mb & 1;
+        if (EPI == EPI_RESIDUAL && mb + 1 < 8) {  // the next m-block's residual in flight
+#pragma unroll
+          for (int p = 0; p < 2; ++p)
+            rq[cur ^ 1][p] = __builtin_amdgcn_raw_buffer_load_b128(rr, rowv + colv[p],
+                                                                   static_cast<uint32_t>((mb + 1) * 16) * ldb, 0);
+        }
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const float a[4] = {acc[2 * p][mb][0], acc[2 * p][mb][1], acc[2 * p][mb][2], acc[2 * p][mb][3]};
+          const float b[4] = {acc[2 * p + 1][mb][0], acc[2 * p + 1][mb][1], acc[2 * p + 1][mb][2],
+                              acc[2 * p + 1][mb][3]};
+          swap_store(mb, colv[p], a, b, bq[p], rq[cur][p]);
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int mb = 0; mb < 8; ++mb) {
     const int m = m0 + g * 128 + mb * 16 + fr;
