@@ -25,14 +25,15 @@ __global__ __launch_bounds__(NORM_THREADS) void add_rmsnorm_kernel(
   const int tid = threadIdx.x;
   const int nvec = H / 8;
   const size_t base = static_cast<size_t>(row) * H;
-  if (gather) x += static_cast<size_t>(gather[row]) * H - base;  // x row = table row gather[row]
+  // x row: table row gather[row] (embedding) or row `row` -- its own pointer, indexed from 0
+  const bf16_t* __restrict__ xr = gather ? x + static_cast<size_t>(gather[row]) * H : x + base;
   float v[MAX_CHUNK][8];
   float ss = 0.f;
 #pragma unroll
   for (int c = 0; c < MAX_CHUNK; ++c) {
     const int vi = tid + c * NORM_THREADS;
     if (vi < nvec) {
-      u16x8 xv = *reinterpret_cast<const u16x8*>(x + base + vi * 8);
+      u16x8 xv = *reinterpret_cast<const u16x8*>(xr + vi * 8);
       u16x8 rv;
       if (has_residual == 1) rv = *reinterpret_cast<const u16x8*>(residual + base + vi * 8);
       u16x8 nr;
