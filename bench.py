@@ -296,8 +296,12 @@ def main(argv=None):
         print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: measuring {world} rank(s)", file=sys.stderr)
 
     # stdout carries exactly ONE line (the JSON result): anything else -- e.g. the
-    # reference's console messages when an agent fails all JSON retries -- goes to stderr
-    result_out, sys.stdout = sys.stdout, sys.stderr
+    # reference's console messages when an agent fails all JSON retries, or native libraries
+    # writing to fd 1 (gloo's "[Gloo] Rank ... connected" lines) -- goes to stderr
+    sys.stdout.flush()
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    sys.stdout = sys.stderr
     if os.environ.get("BCG_STACKS_AFTER"):  # debugging aid: dump every thread's stack periodically
         import faulthandler
         faulthandler.dump_traceback_later(float(os.environ["BCG_STACKS_AFTER"]), repeat=True, file=sys.stderr)
