@@ -27,7 +27,7 @@ def _close(a, b, tol=2e-2):
     assert err <= tol * max(1.0, scale), (err, scale)
 
 
-@pytest.mark.parametrize("cfg", list(range(11)))
+@pytest.mark.parametrize("cfg", list(range(12)))
 @pytest.mark.parametrize("M,N,K", [(37, 256, 512), (200, 768, 1024), (448, 1280, 5120), (1, 256, 128)])
 def test_gemm_store_bias(hip, cfg, M, N, K):
     torch.manual_seed(M + N + cfg)
@@ -42,7 +42,7 @@ def test_gemm_store_bias(hip, cfg, M, N, K):
     _close(yb, _ref(x, w) + b.float())
 
 
-@pytest.mark.parametrize("cfg", list(range(11)))
+@pytest.mark.parametrize("cfg", list(range(12)))
 @pytest.mark.parametrize("M,I,K", [(45, 256, 512), (300, 1024, 1024)])
 def test_gemm_silu_mul_epilogue(hip, cfg, M, I, K):
     torch.manual_seed(I + cfg)
@@ -131,6 +131,24 @@ def test_gemm_pp_edges(hip, M, N, K, epi, cfg):
         _close(got, want)
 
 
+@pytest.mark.parametrize("cfg", [10, 11])
+@pytest.mark.parametrize("M,N,K", [(77, 528, 1024), (1500, 4112, 512)])
+def test_gemm_residual_plus_bias(hip, cfg, M, N, K):
+    """The 256x256 kernels' residual epilogue with a bias as well (both added in fp32), partial
+    tiles in M and N, bf16 and fp8."""
+    torch.manual_seed(M + N + cfg)
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda").to(torch.bfloat16)
+    r = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    want = r.float() + b.float() + _ref(x, w)
+    _close(hip.gemm_nt(x, w, cfg, 2, bias=b, residual=r, out=r), want)
+    xq, xs, wq, ws, ref = _fp8_operands(M, N, K, 3 + cfg)
+    r = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    want = r.float() + b.float() + ref
+    _close(hip.gemm_nt_fp8(xq, xs, wq, ws, cfg, 2, bias=b, residual=r, out=r), want)
+
+
 @pytest.mark.parametrize("M,N,K", [(4096 + 77, 4112, 1024), (16384, 1280, 256), (9000, 2560, 64), (300, 74752, 128)])
 @pytest.mark.parametrize("epi", [0, 1, 2])
 def test_gemm_w4_persistent_many_items(hip, M, N, K, epi):
@@ -179,7 +197,7 @@ def _fp8_operands(M, N, K, seed):
     return xq, xs, wq, ws, ref
 
 
-@pytest.mark.parametrize("cfg", list(range(10)))
+@pytest.mark.parametrize("cfg", list(range(12)))
 @pytest.mark.parametrize("M,N,K", [(37, 256, 512), (200, 768, 1024), (448, 1280, 6144), (1, 256, 128)])
 def test_gemm_fp8_store_bias(hip, cfg, M, N, K):
     bm, bn = hip.gemm_plan.tiles[cfg]
