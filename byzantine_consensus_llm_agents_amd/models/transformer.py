@@ -302,6 +302,22 @@ class DecoderModel:
             return self._forward_fused(tokens, meta, k_cache, v_cache)
         return self._forward_general(tokens, meta, k_cache, v_cache)
 
+    @staticmethod
+    def _last_layer_rows(meta, attn, residual):
+        """Keep only the logits rows after the LAST layer's attention.
+
+        Every row's o_proj / MLP / final norm is independent of the other rows, and past the
+        last attention no later layer reads them: only the rows whose logits are sampled
+        (``meta.logits_idx``, one per prompt that ends in this chunk) need the rest of the
+        layer.  The K/V of every row is already in the cache (written in ``_attention``).
+        In a packed prefill chunk that is the last layer's o / gate_up / down GEMMs on
+        ~10-100 rows instead of up to 16384: ~1/40 of the chunk's GEMM work.  The residual
+        stream of the previous layer is complete here (TP: reduced in this layer's input
+        norm), so selecting it is exact; under TP every rank selects the same rows.
+        """
+        idx = meta.logits_idx
+        return attn.index_select(0, idx), residual.index_select(0, idx)
+
     def _attention(self, li, L, qkv, meta, k_cache, v_cache):
         ops, c = self.ops, self.cfg
         q = ops.qk_norm_rope_kv_write(qkv, meta.positions, meta.slots, self.n_q, self.n_kv, self.hd,
@@ -333,6 +349,7 @@ class DecoderModel:
         fp8, tp1 = self.quant == "fp8", self.tp.size == 1
         eps = c.rms_eps
         residual = x = h = hq = hs = None
+        last = len(self.layers) - 1
         for li, L in enumerate(self.layers):
             # ---- input norm (the previous layer's down projection is reduced here) ----
             if li == 0:
@@ -349,6 +366,8 @@ class DecoderModel:
             qkv = (ops.linear_fp8(hq, hs, L["qkv"], L["qkv_s"], L.get("qkv_bias")) if fp8
                    else ops.linear(h, L["qkv"], L.get("qkv_bias")))
             attn = self._attention(li, L, qkv, meta, k_cache, v_cache)
+            if li == last and meta.logits_idx is not None:  # see _last_layer_rows
+                attn, residual = self._last_layer_rows(meta, attn, residual)
             # ---- o_proj, post-attention norm, MLP ----
             if fp8:
                 aq, as_ = ops.quant_fp8(attn)
@@ -367,10 +386,6 @@ class DecoderModel:
             else:
                 h, residual = tp.all_reduce_add_rmsnorm(ops.linear(attn, L["o"]), residual, L["ln2"], eps, ops)
                 x = ops.linear(ops.linear_silu(h, L["gate_up"]), L["down"])  # partial: reduced at the next norm
-        if meta.logits_idx is not None:
-            residual = residual.index_select(0, meta.logits_idx)
-            if x is not None and not tp1:
-                x = x.index_select(0, meta.logits_idx)
         if tp1 and fp8:
             h = ops.rmsnorm(residual, self.final_norm, eps)
         else:
@@ -391,6 +406,7 @@ class DecoderModel:
         """
         ops, c = self.ops, self.cfg
         residual = None
+        last = len(self.layers) - 1
         for li, L in enumerate(self.layers):
             if li == 0:  # embedding gather fused with the first input norm
                 h, residual = ops.embed_rmsnorm(tokens, self.embed, L["ln1"], c.rms_eps)
@@ -398,11 +414,11 @@ class DecoderModel:
                 h = ops.rmsnorm(residual, L["ln1"], c.rms_eps)
             qkv = ops.linear(h, L["qkv"], L.get("qkv_bias"))
             attn = self._attention(li, L, qkv, meta, k_cache, v_cache)
+            if li == last and meta.logits_idx is not None:  # see _last_layer_rows
+                attn, residual = self._last_layer_rows(meta, attn, residual)
             residual = ops.linear_residual(attn, L["o"], residual)
             h = ops.rmsnorm(residual, L["ln2"], c.rms_eps)
             act = ops.linear_silu(h, L["gate_up"])
             residual = ops.linear_residual(act, L["down"], residual)
-        if meta.logits_idx is not None:
-            residual = residual.index_select(0, meta.logits_idx)
         h = ops.rmsnorm(residual, self.final_norm, c.rms_eps)
         return ops.linear(h, self.lm_head)

@@ -179,3 +179,20 @@ def test_quant_fp8_reference_roundtrip():
     assert (q.float().abs().amax(-1) == 448).all()
     back = q.float() * s[:, None]
     assert ((back - x).abs() <= x.abs().amax(-1, keepdim=True) / 16).all()  # e4m3: 3 mantissa bits
+
+
+@pytest.mark.parametrize("name", ["bcg/tiny-qwen3", "bcg/tiny-mistral"])
+def test_last_layer_row_selection_is_exact(name):
+    """The last layer's o_proj / MLP run on the logits rows only (``_last_layer_rows``): the
+    logits and the KV cache equal a forward that computes every row and selects afterwards."""
+    import dataclasses
+    m = _model(name)
+    tokens, meta, nblk = prefill_batch(SEQS)
+    k1, v1 = alloc_kv(m, nblk)
+    sel = m.forward(tokens, meta, k1, v1)
+    k2, v2 = alloc_kv(m, nblk)
+    full = m.forward(tokens, dataclasses.replace(meta, logits_idx=None), k2, v2)
+    assert full.shape[0] == tokens.shape[0] and sel.shape[0] == len(SEQS)
+    torch.testing.assert_close(sel, full.index_select(0, meta.logits_idx), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(k1, k2, atol=0, rtol=0)
+    torch.testing.assert_close(v1, v2, atol=0, rtol=0)
