@@ -169,32 +169,46 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kv_vec_kernel(
 // gathers its 16 values and writes the block's V^T row d as 32 contiguous bytes -- the
 // per-token form writes 2 bytes at a 32-B stride per element (418 -> 286 us per layer at
 // 16k tokens was left mostly in those stores).  Other groups store element by element.
+//
+// The block is 2*HD threads and both sides move 16 B per lane: thread (i = tid / (HD/8),
+// c = tid % (HD/8)) loads dims 8c..8c+7 of token i (one 16-B load; the former one-thread-per-dim
+// form issued 16 two-byte loads per thread, 128 B per wave instruction, and ran at ~1.4 TB/s),
+// the 16 x HD tile is transposed through LDS, and thread (d = tid / 2, half) stores tokens
+// 8*half..8*half+7 of V^T row d as one 16-B store.
 template <int HD>
-__global__ __launch_bounds__(HD) void v_write_group_kernel(const bf16_t* __restrict__ qkv, const int* __restrict__ slots,
-                                                           bf16_t* __restrict__ v_cache, int layer, int T, int n_q,
-                                                           int n_kv, int num_blocks, int block_size) {
-  const int t0 = blockIdx.x * 16, h = blockIdx.y, d = threadIdx.x;
+__global__ __launch_bounds__(2 * HD) void v_write_group_kernel(const bf16_t* __restrict__ qkv,
+                                                               const int* __restrict__ slots,
+                                                               bf16_t* __restrict__ v_cache, int layer, int T,
+                                                               int n_q, int n_kv, int num_blocks, int block_size) {
+  constexpr int CPT = HD / 8;      // 16-B chunks per token row
+  constexpr int LD = HD + 8;       // LDS row pitch (bf16): rows start 16 B apart in the bank map
+  __shared__ __attribute__((aligned(16))) uint16_t tile[16][LD];
+  const int t0 = blockIdx.x * 16, h = blockIdx.y, tid = threadIdx.x;
   const int nt = min(16, T - t0);
   const int n_heads = n_q + 2 * n_kv;
   const int s0 = slots[t0];
-  const bool mine = d >= nt || slots[t0 + d] == s0 + d;  // thread d < 16 checks token d
+  const bool mine = tid >= nt || slots[t0 + tid] == s0 + tid;  // thread i < 16 checks token i
   const bool fast = __syncthreads_and(mine) && nt == 16 && block_size == 16 && s0 % 16 == 0;
-  const bf16_t* src = qkv + static_cast<size_t>(t0) * n_heads * HD + static_cast<size_t>(n_q + n_kv + h) * HD + d;
+  const bf16_t* head = qkv + static_cast<size_t>(t0) * n_heads * HD + static_cast<size_t>(n_q + n_kv + h) * HD;
   if (fast) {
-    uint32_t w[8];
+    const int i = tid / CPT, c = tid % CPT;
+    const u16x8 x = *reinterpret_cast<const u16x8*>(head + static_cast<size_t>(i) * n_heads * HD + 8 * c);
+    *reinterpret_cast<u16x8*>(&tile[i][8 * c]) = x;
+    __syncthreads();
+    const int d = tid >> 1, half = tid & 1;
+    uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t lo = src[static_cast<size_t>(2 * i) * n_heads * HD];
-      const uint32_t hi = src[static_cast<size_t>(2 * i + 1) * n_heads * HD];
-      w[i] = lo | (hi << 16);
-    }
+    for (int j = 0; j < 4; ++j)
+      w[j] = uint32_t(tile[8 * half + 2 * j][d]) | (uint32_t(tile[8 * half + 2 * j + 1][d]) << 16);
     const int blk = s0 / 16;
-    uint4* dst = reinterpret_cast<uint4*>(
-        v_cache + ((static_cast<size_t>(layer) * num_blocks + blk) * n_kv + h) * HD * 16 + static_cast<size_t>(d) * 16);
-    dst[0] = uint4{w[0], w[1], w[2], w[3]};
-    dst[1] = uint4{w[4], w[5], w[6], w[7]};
+    uint4* dst = reinterpret_cast<uint4*>(v_cache + ((static_cast<size_t>(layer) * num_blocks + blk) * n_kv + h) * HD * 16 +
+                                          static_cast<size_t>(d) * 16 + 8 * half);
+    *dst = uint4{w[0], w[1], w[2], w[3]};
     return;
   }
+  if (tid >= HD) return;  // element-wise path: one thread per dim
+  const int d = tid;
+  const bf16_t* src = head + d;
   for (int i = 0; i < nt; ++i) {
     const int slot = slots[t0 + i];
     const int blk = slot / block_size, off = slot % block_size;
@@ -210,14 +224,17 @@ void launch_vec(const void* qkv, const int* positions, const int* slots, void* q
   constexpr int HPB = 4 * (64 / (HD / 8));  // heads per 256-thread block
   const int n_heads = n_q + 2 * n_kv;
   const bool group_v = std::is_same<CacheT, bf16_t>::value && T >= 64;
-  // (group_v launches only the query/key head blocks when the V heads fill whole blocks)
-  hipLaunchKernelGGL((qk_norm_rope_kv_vec_kernel<CacheT, HD>), dim3(T, (n_heads + HPB - 1) / HPB), dim3(256), 0,
+  // group_v: v_write_group_kernel stores V, so the grid covers the query/key heads only (a
+  // block past them would load its V rows just to return: Qwen3-14B's fourth head block, 2 KB
+  // per token); V heads inside the last query/key block still return early through skip_v
+  const int grid_heads = group_v ? n_q + n_kv : n_heads;
+  hipLaunchKernelGGL((qk_norm_rope_kv_vec_kernel<CacheT, HD>), dim3(T, (grid_heads + HPB - 1) / HPB), dim3(256), 0,
                      stream, static_cast<const bf16_t*>(qkv), positions, slots, static_cast<bf16_t*>(q_out),
                      static_cast<const bf16_t*>(q_norm), static_cast<const bf16_t*>(k_norm), cos_sin,
                      static_cast<CacheT*>(k_cache), static_cast<CacheT*>(v_cache), layer, T, n_q, n_kv, num_blocks,
                      block_size, eps, group_v ? 1 : 0);
   if (group_v)
-    hipLaunchKernelGGL((v_write_group_kernel<HD>), dim3((T + 15) / 16, n_kv), dim3(HD), 0, stream,
+    hipLaunchKernelGGL((v_write_group_kernel<HD>), dim3((T + 15) / 16, n_kv), dim3(2 * HD), 0, stream,
                        static_cast<const bf16_t*>(qkv), slots, reinterpret_cast<bf16_t*>(v_cache), layer, T, n_q,
                        n_kv, num_blocks, block_size);
 }

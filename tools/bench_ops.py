@@ -93,17 +93,18 @@ def main():
     cs = rope_cache(8192, hd, 1e6, "cuda")
     n_q, n_kv = cfg.num_heads, cfg.num_kv_heads
     out["rope"] = []
-    for T in (616, 16384):
+    for T, in_order in ((616, False), (16384, False), (16384, True)):  # in order: a prefill chunk's blocks
         nbk = T // 16 + 2
         kc = torch.zeros(1, nbk, n_kv, 16, hd, device="cuda", dtype=torch.bfloat16)
         vc = torch.zeros(1, nbk, n_kv, hd, 16, device="cuda", dtype=torch.bfloat16)
         qkv = torch.randn(T, (n_q + 2 * n_kv) * hd, device="cuda", dtype=torch.bfloat16)
         pos = torch.randint(0, 4000, (T,), device="cuda", dtype=torch.int32)
-        slots = torch.randperm(nbk * 16, device="cuda")[:T].to(torch.int32)
+        slots = (torch.arange(16, 16 + T, device="cuda") if in_order
+                 else torch.randperm(nbk * 16, device="cuda")[:T]).to(torch.int32)
         wn = torch.ones(hd, device="cuda", dtype=torch.bfloat16)
         t = timeit(lambda: hip.qk_norm_rope_kv_write(qkv, pos, slots, n_q, n_kv, hd, wn, wn, 1e-6, cs, kc, vc, 0))
         gb = (qkv.numel() * 2 + T * n_q * hd * 2 + T * 2 * n_kv * hd * 2) / 1e9
-        rec = {"T": T, "rope_us": round(t, 1), "TBps": round(gb / t * 1e3, 2)}
+        rec = {"T": T, "in_order": in_order, "rope_us": round(t, 1), "TBps": round(gb / t * 1e3, 2)}
         out["rope"].append(rec)
         print(json.dumps(rec), flush=True)
     # sampler
