@@ -94,17 +94,15 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kv_kernel(
 // moved 2 bytes per lane per access and was latency-bound at decode sizes (34 us per layer
 // at 616 rows, ~10x its byte time).
 template <typename CacheT, int HD>
-__global__ __launch_bounds__(256) void qk_norm_rope_kv_vec_kernel(
-    const bf16_t* __restrict__ qkv, const int* __restrict__ positions, const int* __restrict__ slots,
+__device__ __forceinline__ void rope_kv_token(
+    int t, const bf16_t* __restrict__ qkv, const int* __restrict__ positions, const int* __restrict__ slots,
     bf16_t* __restrict__ q_out, const bf16_t* __restrict__ q_norm, const bf16_t* __restrict__ k_norm,
     const float* __restrict__ cos_sin, CacheT* __restrict__ k_cache, CacheT* __restrict__ v_cache,
-    int layer, int T, int n_q, int n_kv, int num_blocks, int block_size, float eps, int skip_v) {
+    int layer, int n_q, int n_kv, int num_blocks, int block_size, float eps, int skip_v) {
   constexpr int HALF = HD / 2, LPH = HALF / 4, HPW = 64 / LPH;  // lanes per head, heads per wave
   const int lane = threadIdx.x & 63, li = lane % LPH;
   const int slot_head = (blockIdx.y * 4 + (threadIdx.x >> 6)) * HPW + lane / LPH;
-  const int t = blockIdx.x;
   const int n_heads = n_q + 2 * n_kv;
-  if (t >= T) return;
   const bool valid = slot_head < n_heads;  // idle lanes still take part in the shuffles
   const int d0 = 4 * li;
   const bf16_t* src = qkv + (static_cast<size_t>(t) * n_heads + (valid ? slot_head : 0)) * HD;
@@ -162,6 +160,22 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kv_vec_kernel(
       dst[HALF + d0 + e] = to_cache<CacheT>(y2[e]);
     }
   }
+}
+
+// ROPE_TPB consecutive tokens per workgroup: a prefill chunk launched one token per workgroup
+// was ~49k workgroups of 8 KB each (Qwen3-14B, 16k tokens) -- dispatch-bound, not byte-bound.
+constexpr int ROPE_TPB = 4;
+
+template <typename CacheT, int HD>
+__global__ __launch_bounds__(256) void qk_norm_rope_kv_vec_kernel(
+    const bf16_t* __restrict__ qkv, const int* __restrict__ positions, const int* __restrict__ slots,
+    bf16_t* __restrict__ q_out, const bf16_t* __restrict__ q_norm, const bf16_t* __restrict__ k_norm,
+    const float* __restrict__ cos_sin, CacheT* __restrict__ k_cache, CacheT* __restrict__ v_cache,
+    int layer, int T, int n_q, int n_kv, int num_blocks, int block_size, float eps, int skip_v, int tpb) {
+  const int t0 = blockIdx.x * tpb, t1 = min(T, t0 + tpb);
+  for (int t = t0; t < t1; ++t)  // block-uniform
+    rope_kv_token<CacheT, HD>(t, qkv, positions, slots, q_out, q_norm, k_norm, cos_sin, k_cache, v_cache, layer,
+                              n_q, n_kv, num_blocks, block_size, eps, skip_v);
 }
 
 // Prefill V (T >= 64): one workgroup per (16 consecutive tokens, kv head), one thread per dim.
@@ -228,11 +242,13 @@ void launch_vec(const void* qkv, const int* positions, const int* slots, void* q
   // block past them would load its V rows just to return: Qwen3-14B's fourth head block, 2 KB
   // per token); V heads inside the last query/key block still return early through skip_v
   const int grid_heads = group_v ? n_q + n_kv : n_heads;
-  hipLaunchKernelGGL((qk_norm_rope_kv_vec_kernel<CacheT, HD>), dim3(T, (grid_heads + HPB - 1) / HPB), dim3(256), 0,
+  const int tpb = T >= 1024 ? ROPE_TPB : 1;  // decode rows keep one token per workgroup (parallelism)
+  hipLaunchKernelGGL((qk_norm_rope_kv_vec_kernel<CacheT, HD>), dim3((T + tpb - 1) / tpb, (grid_heads + HPB - 1) / HPB),
+                     dim3(256), 0,
                      stream, static_cast<const bf16_t*>(qkv), positions, slots, static_cast<bf16_t*>(q_out),
                      static_cast<const bf16_t*>(q_norm), static_cast<const bf16_t*>(k_norm), cos_sin,
                      static_cast<CacheT*>(k_cache), static_cast<CacheT*>(v_cache), layer, T, n_q, n_kv, num_blocks,
-                     block_size, eps, group_v ? 1 : 0);
+                     block_size, eps, group_v ? 1 : 0, tpb);
   if (group_v)
     hipLaunchKernelGGL((v_write_group_kernel<HD>), dim3((T + 15) / 16, n_kv), dim3(2 * HD), 0, stream,
                        static_cast<const bf16_t*>(qkv), slots, reinterpret_cast<bf16_t*>(v_cache), layer, T, n_q,
