@@ -92,8 +92,6 @@ def parse(argv=None):
                     help="fp8 halves KV bytes (reduced precision: never used for the bf16 headline)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
-    ap.add_argument("--overlap-prefill", action="store_true",
-                    help="prefill on a second HIP stream, concurrent with decode bursts (TP=1)")
     ap.add_argument("--no-custom-allreduce", action="store_true",
                     help="TP collectives through RCCL only (no xGMI one-/two-shot kernels)")
     ap.add_argument("--kv-cache-gb", type=float, default=None,
@@ -120,8 +118,7 @@ def self_launch(args) -> int:
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", BCG_BENCH_T0=repr(time.time() - (time.perf_counter() - T_PROCESS0)))
-    env.setdefault("OMP_NUM_THREADS", "4")
-    return subprocess.call(cmd, env=env)
+    return subprocess.call(cmd, env=env)  # (each rank sets its own thread budget: rank_thread_budget)
 
 
 class SimPool:
@@ -141,6 +138,7 @@ class SimPool:
         self.generation = [0] * n_sims
         self.sims = [self._new_sim(i) for i in range(n_sims)]
         self.retired = 0          # accepted decisions of games already replaced
+        self.retired_counters = {}  # every simulation counter of games already replaced
         self.games_finished = 0
         self.game_rounds = []     # rounds played by each finished game (burn-in rounds included)
         self.engine_rounds = []   # ... of them on the engine (burn-in rounds excluded)
@@ -213,6 +211,16 @@ class SimPool:
         with self.lock:
             return self.retired + sum(self._made(s) for s in self.sims)
 
+    def counter_totals(self) -> dict:
+        """Every simulation counter (accepted outputs, retry-ladder calls, rows, exhausted
+        outputs) summed over every game this pool played."""
+        with self.lock:
+            tot = dict(self.retired_counters)
+            for s in self.sims:
+                for k, v in s.counters.items():
+                    tot[k] = tot.get(k, 0) + v
+            return tot
+
     def _work(self, i, delay):
         try:
             if delay > 0 and self._stop.wait(delay):
@@ -231,6 +239,8 @@ class SimPool:
                         self.game_rounds.append(played)
                         self.engine_rounds.append(played - (self.ages[i] if self.generation[i] == 1 else 0))
                         self.retired += self._made(sim)
+                        for k, v in sim.counters.items():
+                            self.retired_counters[k] = self.retired_counters.get(k, 0) + v
                         self.sims[i] = fresh
         except BaseException as exc:  # surfaced by the main thread
             self.errors.append(exc)
@@ -270,6 +280,72 @@ def window_stats(per_window, window_s: float):
     return out
 
 
+RETRY_KEYS = ("decide_prompts", "vote_prompts", "decide_batches", "vote_batches", "batch_rows",
+              "sequential_calls", "sequential_attempts", "decisions_exhausted", "votes_exhausted")
+
+
+def retry_summary(delta: dict) -> dict:
+    """Timed-region cost of the retry ladder (retries count toward time, not toward
+    decisions): prompts the games asked for, rows the engine generated for them (batch rows incl.
+    re-batched failures + the agents' own sequential attempts), and outputs that exhausted every
+    attempt.  `engine_rows_per_prompt` - 1 is the generation work retries added."""
+    out = {k: int(delta.get(k, 0)) for k in RETRY_KEYS}
+    prompts = out["decide_prompts"] + out["vote_prompts"]
+    rows = out["batch_rows"] + out["sequential_attempts"]
+    out["retry_rows"] = rows - prompts
+    out["engine_rows_per_prompt"] = round(rows / prompts, 4) if prompts else None
+    return out
+
+
+def thread_cpu():
+    """{native thread id: (group, CPU seconds)} of this process's live threads.  Groups: the game
+    threads (`sim*`), the engine's scheduler thread, the main thread, other Python threads, and
+    threads with no Python name (HIP runtime, the tokenizer's rayon pool, gloo)."""
+    try:
+        import psutil
+    except ImportError:
+        return {}
+    names = {t.native_id: t.name for t in threading.enumerate()}
+
+    def group(name):
+        if name is None:
+            return "native"
+        if name.startswith("sim"):
+            return "game_threads"
+        if name.startswith("bcg-engine") or name.startswith("bcg-tp"):
+            return "engine"
+        return "main" if name == "MainThread" else "python_other"
+    return {t.id: (group(names.get(t.id)), t.user_time + t.system_time) for t in psutil.Process().threads()}
+
+
+def thread_cpu_delta(before: dict, after: dict, total_s: float) -> dict:
+    """CPU seconds per thread group between two `thread_cpu` snapshots; threads that ended in
+    between (the short-lived sequential-retry threads) show up as `unattributed`."""
+    out = {}
+    for tid, (grp, t) in after.items():
+        out[grp] = out.get(grp, 0.0) + t - before.get(tid, (grp, 0.0))[1]
+    out = {k: round(v, 1) for k, v in sorted(out.items())}
+    out["unattributed"] = round(total_s - sum(out.values()), 1)
+    return out
+
+
+def rank_thread_budget(world: int) -> int:
+    """Host threads per rank for the tokenizer's rayon pool, OpenMP and torch's CPU ops: this
+    process's CPUs split over the node's ranks (without it every rank's pools
+    default to every logical CPU of the node).  An explicit RAYON_NUM_THREADS / OMP_NUM_THREADS
+    in the environment wins."""
+    try:
+        cpus = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cpus = os.cpu_count() or 8
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", world) or world)
+    per = max(2, min(16, cpus // max(1, local)))
+    os.environ.setdefault("RAYON_NUM_THREADS", str(per))
+    os.environ.setdefault("OMP_NUM_THREADS", str(per))
+    os.environ.setdefault("TOKENIZERS_PARALLELISM", "true")
+    return per
+
+
 def _heartbeat(llm, pool, stop: threading.Event, every: float = 30.0):
     """Progress line on stderr every `every` s (long runs must keep writing)."""
     t0 = time.perf_counter()
@@ -292,6 +368,7 @@ def main(argv=None):
         t_origin = T_PROCESS0
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    host_threads = rank_thread_budget(world)  # before torch / tokenizers start their pools
     if args.gpus != world and rank == 0:
         print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: measuring {world} rank(s)", file=sys.stderr)
 
@@ -308,6 +385,7 @@ def main(argv=None):
 
     import torch
     import torch.distributed as dist
+    torch.set_num_threads(min(torch.get_num_threads(), host_threads))
 
     gpu = args.backend == "hip"
     if args.backend == "hostmodel":
@@ -339,7 +417,7 @@ def main(argv=None):
     C.VLLM_CONFIG["quantization"] = args.quantization
     C.ENGINE_CONFIG.update(backend=args.backend, budget_aware_json=True, seed=args.seed + replica,
                            use_hip_graphs=not args.no_graphs, prefix_caching=not args.no_prefix_cache,
-                           overlap_prefill=args.overlap_prefill, custom_allreduce=not args.no_custom_allreduce,
+                           custom_allreduce=not args.no_custom_allreduce,
                            kv_cache_dtype=args.kv_cache_dtype)
     if C.ENGINE_CONFIG.get("num_layers_override"):
         raise SystemExit("bench.py: num_layers_override (reduced depth) is a test option, never a measurement")
@@ -418,6 +496,8 @@ def main(argv=None):
         torch.cuda.synchronize()
     t_start = time.perf_counter()
     cpu0 = time.process_time()  # this rank's host CPU (all threads) over the timed region
+    thr0 = thread_cpu()
+    ctr0 = pool.counter_totals() if pool is not None else {}
     a0 = accepted()
     per_window, steps_done, last = [], 0, a0
 
@@ -442,11 +522,15 @@ def main(argv=None):
         tok_last = t_now
         steps_done += 1
     decisions = last - a0
-    host_cpu_s = time.process_time() - cpu0
+    ctr1 = pool.counter_totals() if pool is not None else {}
     if gpu:
         torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t_start
+    # (bookkeeping after the clock stops: none of it inside the timed region)
+    host_cpu_s = time.process_time() - cpu0
+    threads_cpu = thread_cpu_delta(thr0, thread_cpu(), host_cpu_s)
+    retry_delta = [float(ctr1.get(k, 0) - ctr0.get(k, 0)) for k in RETRY_KEYS]
     if rank == 0:
         print(f"[timed] {steps_done} windows decisions={decisions} elapsed={elapsed:.2f}s", file=sys.stderr,
               flush=True)
@@ -473,6 +557,20 @@ def main(argv=None):
         dist.all_reduce(tt, op=dist.ReduceOp.SUM, group=ctrl)
         tok = float(tt[0])
     tokens_per_s = tok / elapsed if elapsed > 0 else 0.0
+    if world > 1:  # retry-ladder counters summed over the DP replicas' pools
+        rt = torch.tensor(retry_delta, dtype=torch.float64)
+        dist.all_reduce(rt, op=dist.ReduceOp.SUM, group=ctrl)
+        retry_delta = rt.tolist()
+    retry = retry_summary(dict(zip(RETRY_KEYS, retry_delta)))
+    # the layout as every rank saw it: which ranks drive a game pool (one per DP replica, its own
+    # seeds) and which only execute their TP driver's plans
+    me = {"rank": rank, "replica": replica, "driver": pool is not None,
+          "seed_base": pool.seed_base if pool is not None else None,
+          "sims": len(pool.sims) if pool is not None else 0, "decisions": decisions if pool is not None else 0}
+    ranks = [me]
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me, group=ctrl)
     # host budget: CPU seconds of every rank's process over the timed region (summed) and the
     # slowest DP replica's decision rate
     per_rank_rate = decisions / elapsed if elapsed > 0 and pool is not None else float("inf")
@@ -505,7 +603,6 @@ def main(argv=None):
                        "step": f"{args.window_s:g} s window of the continuously-batched pool",
                        "parallelism": f"dp{world // args.tp}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
                        "hip_graphs": not args.no_graphs, "prefix_caching": not args.no_prefix_cache,
-                       "overlap_prefill": args.overlap_prefill,
                        "custom_allreduce": args.tp > 1 and not args.no_custom_allreduce},
             "detail": {"decisions": total_decisions, "elapsed_s": round(elapsed, 3), "init_s": round(init_s, 1),
                        "steps_requested": args.steps, "window_s": args.window_s,
@@ -518,7 +615,13 @@ def main(argv=None):
                        # the same spread for the engine's token count per window: the smooth
                        # series A/B comparisons should use
                        "token_window_stats_rank0": window_stats(tok_windows, args.window_s),
+                       "retry": retry,
+                       "ranks": ranks,
                        "host": {"cpu_s_all_ranks": round(host_cpu_s, 1),
+                                # rank 0's CPU seconds by thread group over the timed region
+                                "cpu_s_by_thread_rank0": threads_cpu,
+                                "threads_per_rank": host_threads,
+                                "rayon_threads": os.environ.get("RAYON_NUM_THREADS"),
                                 "cpu_s_per_decision": (round(host_cpu_s / total_decisions, 4)
                                                        if total_decisions else None),
                                 "min_replica_decisions_per_s": round(per_rank_rate, 3),

@@ -214,6 +214,7 @@ class BCGAgent(EngineAgent):
         prompt = base_prompt
         result = None
         for attempt in range(1, MAX_JSON_RETRIES + 1):
+            self.sequential_attempts = getattr(self, "sequential_attempts", 0) + 1  # (retry cost counter)
             result = self.generate_json(prompt, schema, temperature=temperature,
                                         max_tokens=max_tokens, system_prompt=system_prompt)
             verbose_print(f"🔍 [{self.agent_id} attempt {attempt}] {json.dumps(result)}")

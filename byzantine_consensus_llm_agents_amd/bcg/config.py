@@ -98,11 +98,6 @@ ENGINE_CONFIG = {
     # only while >= admit_min_live rows decode.  3 vs 0, two A/B pairs on one GPU: 31.0k / 31.5k
     # vs 30.6k / 30.8k tokens/s (profiles/bench_r2_ab*_a*.json)
     "admit_max_wait": int(os.environ.get("BCG_ADMIT_MAX_WAIT", "3")),
-    # prefill on a second HIP stream, overlapped with decode bursts (single-GPU / DP ranks).
-    # Off by default: measured no gain at 32 sims/GPU (19.2 vs 19.1 decisions/s), and
-    # hipBLASLt's stream-K prefill GEMMs (inter-workgroup waits) beside a second
-    # persistent kernel can starve each other -- one run hung.
-    "overlap_prefill": os.environ.get("BCG_OVERLAP_PREFILL", "0") == "1",
     # tests only: run the model with this many decoder layers (real layer shapes, reduced depth)
     "num_layers_override": None,
 }

@@ -161,8 +161,13 @@ class BCGSimulation:
         self.log_buffer: List[str] = []
         self.verbose = config.get("verbose", False) if config else False
         self._log_file = None
+        # accepted outputs (the headline metric) and the retry ladder's cost: engine calls,
+        # rows sent to batch calls (first attempts + re-batched failures), sequential
+        # re-queries, and outputs that exhausted every attempt (abstain / default CONTINUE)
         self.counters = {"decisions_accepted": 0, "votes_accepted": 0,
-                         "decide_batches": 0, "vote_batches": 0, "sequential_calls": 0}
+                         "decide_batches": 0, "vote_batches": 0, "sequential_calls": 0,
+                         "decide_prompts": 0, "vote_prompts": 0, "batch_rows": 0,
+                         "sequential_attempts": 0, "decisions_exhausted": 0, "votes_exhausted": 0}
 
         json_dir = os.path.join(METRICS_CONFIG["results_dir"], "json")
         if METRICS_CONFIG.get("save_results", True):
@@ -240,6 +245,10 @@ class BCGSimulation:
         return is_valid_vote(result)
 
     # ------------------------------------------------------- retry ladder
+    def _attempts(self, pending) -> int:
+        """Engine calls the agents' own sequential retry loops have made so far."""
+        return sum(getattr(self.agents[aid], "sequential_attempts", 0) for aid, _ in pending)
+
     def _ladder(self, jobs: List[Tuple[str, tuple]], temperature: float, max_tokens: int,
                 valid, sequential, kind: str) -> Dict[str, Optional[Dict]]:
         """Shared batch-then-sequential retry policy for both phases."""
@@ -247,6 +256,7 @@ class BCGSimulation:
         if not jobs:
             return results
         engine = next(iter(self.agents.values()))
+        self.counters["decide_prompts" if kind == "agents" else "vote_prompts"] += len(jobs)
         pending = list(jobs)
         for attempt in range(1, MAX_RETRIES + 1):
             if not pending:
@@ -256,6 +266,7 @@ class BCGSimulation:
             else:
                 self.log(f"  [RETRY {attempt}/{MAX_RETRIES}] Retrying {len(pending)} failed {kind}...")
             self.counters["decide_batches" if kind == "agents" else "vote_batches"] += 1
+            self.counters["batch_rows"] += len(pending)
             outs = engine.batch_generate_json([p for _, p in pending], temperature=temperature,
                                               max_tokens=max_tokens)
             failed = []
@@ -287,8 +298,10 @@ class BCGSimulation:
 
         def sequential(pending, results):
             self.counters["sequential_calls"] += len(pending)
+            before = self._attempts(pending)
             values = run_concurrently(self._engine_agent(), [
                 (lambda a=self.agents[aid]: a.decide_next_value(game_state)) for aid, _ in pending])
+            self.counters["sequential_attempts"] += self._attempts(pending) - before
             still = []
             for (aid, prompt), value in zip(pending, values):
                 if value is not None:
@@ -307,6 +320,7 @@ class BCGSimulation:
             agent = self.agents[aid]
             res = results.get(aid)
             if res is None:
+                self.counters["decisions_exhausted"] += 1
                 agent.last_reasoning = f"⚠️ All {MAX_RETRIES} attempts failed - abstaining"
                 self.log(f"  {aid}: ABSTAINING (all attempts failed)")
                 continue
@@ -327,8 +341,10 @@ class BCGSimulation:
 
         def sequential(pending, results):
             self.counters["sequential_calls"] += len(pending)
+            before = self._attempts(pending)
             votes = run_concurrently(self._engine_agent(), [
                 (lambda a=self.agents[aid]: a.vote_to_terminate(game_state)) for aid, _ in pending])
+            self.counters["sequential_attempts"] += self._attempts(pending) - before
             for (aid, _), vote in zip(pending, votes):
                 results[aid] = {"_sequential_success": True, "vote": vote,
                                 "_valid": getattr(self.agents[aid], "last_vote_valid", True)}
@@ -344,6 +360,7 @@ class BCGSimulation:
         for aid, _ in jobs:
             res = results.get(aid)
             if res is None:
+                self.counters["votes_exhausted"] += 1
                 vote = False
                 self.log(f"  {aid}: votes CONTINUE (default - all attempts failed)")
             else:
@@ -351,6 +368,8 @@ class BCGSimulation:
                 # the game sees it exactly as the reference does, the counter does not
                 if res.get("_valid", True):
                     self.counters["votes_accepted"] += 1
+                else:
+                    self.counters["votes_exhausted"] += 1
                 if res.get("_sequential_success"):
                     vote = res.get("vote", False)
                 else:

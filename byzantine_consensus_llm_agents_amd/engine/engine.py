@@ -88,7 +88,6 @@ class EngineArgs:
     device: Optional[str] = None
     poll_every: int = 8
     async_mode: bool = False
-    overlap_prefill: bool = False  # prefill on its own HIP stream, concurrent with decode bursts
     precapture_graphs: bool = True  # capture every decode bucket at the first burst (and after FSM growth)
     kv_cache_dtype: str = "auto"    # "auto" = activation dtype (bf16); "fp8" = OCP e4m3fn (half the KV bytes)
     # admission batching (0 = admit at once): queue prompts for up to this many decode
@@ -123,7 +122,6 @@ class EngineArgs:
                    use_hip_graphs=ec.get("use_hip_graphs", True),
                    kv_cache_gb=ec.get("kv_cache_gb"),
                    honor_max_num_seqs=ec.get("honor_max_num_seqs", False),
-                   overlap_prefill=ec.get("overlap_prefill", False),
                    precapture_graphs=ec.get("precapture_graphs", True),
                    kv_cache_dtype=ec.get("kv_cache_dtype", "auto"),
                    admit_max_wait=int(ec.get("admit_max_wait", 0)),
@@ -207,22 +205,12 @@ class InferenceEngine:
         self._stop = False
         self._ar_err_host = None
         self.graphs = None
-        # Prefill (MFMA-bound GEMMs) runs on a second stream while decode bursts
-        # (HBM-bound) keep replaying on the main stream.  Off under TP: RCCL
-        # collectives of one communicator must not run on two streams at once.
-        self.overlap = bool(args.overlap_prefill and self.device.type == "cuda" and self.tp.size == 1)
-        self.prefill_stream = torch.cuda.Stream(self.device) if self.overlap else None
+        # Prefill runs on the engine's one stream between decode bursts.  (A second prefill
+        # stream concurrent with the bursts lost three A/Bs, the last -2.9 % tokens/s: every
+        # 256x256 GEMM holds a CU's whole LDS, so the two streams only time-share the CUs --
+        # PERF.md "Overlapped prefill"; removed in round 5.)
         if hasattr(self.ops, "prepare_device"):  # split-K counters: allocated before any graph capture
             self.ops.prepare_device(self.device)
-            if self.prefill_stream is not None:
-                self.ops.register_stream(self.prefill_stream)
-        self._saved_avoid_library = None
-        if self.overlap and hasattr(self.ops, "gemm_plan"):
-            # no stream-K library GEMM may run beside the other stream's kernels (ops/gemm_plan.py);
-            # the ops namespace is process-wide: restored by shutdown()
-            self._saved_avoid_library = self.ops.gemm_plan.avoid_library
-            self.ops.gemm_plan.avoid_library = True
-        self._inflight = None
         self._bursts = 0         # decode bursts launched (admission-batching clock)
         self._snap = None        # host copy of (done, gen_count, out_tokens) after the last burst
         self._engine_errors = 0
@@ -460,7 +448,6 @@ class InferenceEngine:
                 raise
 
     def _fail_all(self, exc):
-        self._inflight = None
         self._snap = None
         with self._cv:
             pending = list(self._incoming) + list(self._waiting)
@@ -568,10 +555,7 @@ class InferenceEngine:
             self._decode_burst()
             launched = True
         self._reap()
-        if self._inflight is not None and (not self._live_rows() or self._inflight["event"].query()):
-            self._finish_prefill()
-        if self._inflight is None:
-            self._admit()
+        self._admit()
         if not launched and self._live_rows():
             self._decode_burst()
         self._take_snapshot()
@@ -656,41 +640,19 @@ class InferenceEngine:
             if not admitted and not any(self.slots) and self._waiting:
                 raise RuntimeError("KV cache too small for a single waiting sequence")
         if admitted:
-            self._launch_prefill(admitted)
-            if not self.overlap:
-                self._finish_prefill()
+            self._prefill(admitted)
 
-    def _launch_prefill(self, reqs: List["_Request"]):
-        """Enqueue the prompts' prefill; with overlap on the prefill stream, without blocking the host.
-
-        The new rows stay parked (done, scratch block) in the decode state until
-        `_finish_prefill`, so bursts replayed meanwhile leave them untouched.
-        """
+    def _prefill(self, reqs: List["_Request"]):
+        """Prefill the admitted prompts, then activate them: write their state rows, commit the
+        prompt blocks, sample token 1."""
         seqs = [r.seq for r in reqs]
         table_cpu = self._block_table(seqs, len(seqs))
-        stream = self.prefill_stream
-        ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
-        if stream is not None:
-            stream.wait_stream(torch.cuda.current_stream())
-        with self.timer.phase("prefill"), ctx:
+        with self.timer.phase("prefill"):
             plans = self._plan_prefill(seqs, table_cpu)
             logits = self._run_prefill(plans, len(seqs))
-            event = torch.cuda.Event() if stream is not None else None
-            if event is not None:
-                event.record(stream)
-        self._inflight = {"reqs": reqs, "table": table_cpu, "logits": logits, "event": event}
-
-    def _finish_prefill(self):
-        """Activate the in-flight wave: write its state rows, commit prompt blocks, sample token 1."""
-        fl, self._inflight = self._inflight, None
-        reqs, logits = fl["reqs"], fl["logits"]
-        if fl["event"] is not None:
-            torch.cuda.current_stream().wait_event(fl["event"])
-            logits.record_stream(torch.cuda.current_stream())
-        st, dev = self.state, self.device
-        seqs = [r.seq for r in reqs]
+        st = self.state
         rows_d = self._h2d(torch.tensor([r.row for r in reqs], dtype=torch.long))
-        st["block_tables"].index_copy_(0, rows_d, self._h2d(fl["table"]))
+        st["block_tables"].index_copy_(0, rows_d, self._h2d(table_cpu))
         vals = {"seq_lens": [len(s.prompt_ids) for s in seqs], "fsm_base": [s.fsm_base for s in seqs],
                 "fsm_state": [0] * len(seqs), "gen_count": [0] * len(seqs),
                 "max_new": [s.max_new for s in seqs], "row_keys": [self._next_key() for _ in seqs],
@@ -936,9 +898,6 @@ class InferenceEngine:
         if self._follower is not None:
             self._follower.join(timeout=120)
             self._follower = None
-        if self._saved_avoid_library is not None:
-            self.ops.gemm_plan.avoid_library = self._saved_avoid_library
-            self._saved_avoid_library = None
         self.graphs = None
         self.k_cache = self.v_cache = None
         self.model = None

@@ -101,7 +101,7 @@ class FaultInjector:
     "decide"|"vote", "tries": [1, 2], "mode": "invalid_json"|"short"|"exception"}``.
     ``tries`` counts the requests of that (agent, round, phase) in the order
     they are made -- batched attempts, then the sequential attempts (whose
-    prompts carry the ``RETRY ATTEMPT k/3`` suffix).  The reference and this
+    prompts carry the ``RETRY ATTEMPT k/3`` suffix); ``"all"`` fails every one.  The reference and this
     framework send every agent's requests in the same order, whatever the
     batching, so the same plan fails the same requests on both sides:
 
@@ -135,7 +135,7 @@ class FaultInjector:
         self.tries[key] += 1
         t = self.tries[key]
         for rule in self.plan:
-            if (rule["agent"], rule["round"], rule["phase"]) == key and t in rule["tries"]:
+            if (rule["agent"], rule["round"], rule["phase"]) == key and (rule["tries"] == "all" or t in rule["tries"]):
                 return rule["mode"]
         return None
 

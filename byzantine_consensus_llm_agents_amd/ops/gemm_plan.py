@@ -13,13 +13,6 @@ simple rule (hand kernel up to ``max_m`` rows).
 ``force`` = hand kernel wherever the shape is supported (tests; ``BCG_HAND_GEMM_SPLIT``
 = the split-K to force with it).
 
-``avoid_library`` (set by the engine when prefill overlaps decode on a second
-stream): every supported shape runs a hand kernel -- the fastest measured hand
-configuration, else the 256x256 kernel.  hipBLASLt's stream-K kernels (``SK3``,
-picked for the wide decode GEMMs) make workgroups wait for partial tiles of
-other workgroups of the same launch; two such launches on two streams can each
-hold CUs the other's waiting workgroups need (PERF.md, "Overlapped prefill").
-The hand kernels never wait on another workgroup (split-K: last arriver reduces).
 """
 
 import ctypes
@@ -43,7 +36,6 @@ class GemmPlan:
         self.mode = os.environ.get("BCG_HAND_GEMM", "1")
         self.force_split = int(os.environ.get("BCG_HAND_GEMM_SPLIT", "1"))  # split-K in "force" mode (tests)
         self.max_m = max_m
-        self.avoid_library = False
         self.timings: Dict[Tuple[int, int, int, int], Dict[str, float]] = {}
         self.tiles = {}
         for cfg in range(N_CFGS):
@@ -66,9 +58,11 @@ class GemmPlan:
         if cfg not in self.tiles or M <= 0 or K % 64 or K <= 0 or split_k < 1 or K // 64 < split_k:
             return False
         bn = self.tiles[cfg][1]
-        if cfg in BIG_CFGS:  # 32-bit buffer offsets: operands below 4 GiB (W4: 2 GiB)
+        if cfg in BIG_CFGS:  # 32-bit buffer offsets: operands below 4 GiB (W4: 2 GiB), output below 2 GiB
             lim = 1 << (31 if cfg == W4_CFG else 32)
+            ldc = N // 2 if epi == 1 else N
             return (N % 16 == 0 and 2 * (M + 256) * K < lim and 2 * (N + 256) * K < lim
+                    and 2 * (M + 256) * ldc < 1 << 31
                     and (epi != 1 or (N % 2 == 0 and (N // 2) % 128 == 0)))
         if N % bn:
             return False
@@ -78,20 +72,6 @@ class GemmPlan:
 
     def default_cfg(self, M: int) -> int:
         return 1 if M <= 64 else 0
-
-    def _best_hand(self, M: int, N: int, K: int, epi: int) -> Optional[Tuple[int, int]]:
-        """Fastest measured hand configuration of the nearest measured M >= M, else the 256x256 kernel."""
-        above = [m for (m, n, k, e) in self.timings if (n, k, e) == (N, K, epi) and m >= M]
-        if above:
-            times = self.timings[(min(above), N, K, epi)]
-            for name, _ in sorted(((n_, t) for n_, t in times.items() if n_ != "lib" and t), key=lambda kv: kv[1]):
-                cfg, split = map(int, name.split("x"))
-                if self.supported(cfg, M, N, K, epi, split):
-                    return (cfg, split)
-        if self.supported(PP_CFG, M, N, K, epi):
-            return (PP_CFG, 1)
-        cfg = self.default_cfg(M)
-        return (cfg, 1) if self.supported(cfg, M, N, K, epi) else None
 
     def _lookup(self, M: int, N: int, K: int, epi: int) -> Optional[Tuple[int, int]]:
         """Table choice at M, else at the nearest measured M above (same projection shape)."""
@@ -106,8 +86,6 @@ class GemmPlan:
         """(tile configuration, split-K) of the hand kernel, or None for the library path."""
         if self.mode == "0":
             return None
-        if self.avoid_library:
-            return self._best_hand(M, N, K, epi)
         if self.mode == "force":
             for cfg in (self.default_cfg(M),) + tuple(range(N_CFGS)):
                 for split in ((self.force_split, 1) if self.force_split > 1 else (1,)):
@@ -160,9 +138,10 @@ class Fp8Plan:
         if cfg < 0 or cfg not in self.tiles or K // 128 < split:
             return None
         if cfg == PP_CFG:  # 256 x 256 ping-pong fp8 kernel (prefill M): N % 16, 32-bit buffer offsets
-            ok = N % 16 == 0 and M * K < 1 << 32 and N * K < 1 << 32
+            ok = N % 16 == 0 and M * K < 1 << 32 and N * K < 1 << 32 and 2 * (M + 256) * N < 1 << 31
         elif cfg == W4_CFG:  # four-wave 256 x 256 fp8 kernel: N % 16, offsets below 2 GiB
-            ok = N % 16 == 0 and (M + 256) * K < 1 << 31 and (N + 256) * K < 1 << 31
+            ok = (N % 16 == 0 and (M + 256) * K < 1 << 31 and (N + 256) * K < 1 << 31
+                  and 2 * (M + 256) * N < 1 << 31)
         else:
             ok = N % self.tiles[cfg][1] == 0
         return (cfg, split) if ok else None

@@ -246,9 +246,8 @@ def hip_ops() -> SimpleNamespace:
     # tile resets its counter, so a buffer stays zero between launches).  Kernels that may
     # run CONCURRENTLY need disjoint buffers: one per device for the engine's main stream --
     # shared by eager launches and every captured decode graph, which replay on that stream
-    # one after another -- and one per registered side stream (the overlapped-prefill
-    # stream).  Buffers are allocated eagerly by `prepare_device` / `register_stream`, never
-    # inside a graph capture: a zero-fill captured into one bucket's graph would leave the
+    # one after another -- and one per registered side stream.  Buffers are allocated eagerly
+    # by `prepare_device` / `register_stream`, never inside a graph capture: a zero-fill captured into one bucket's graph would leave the
     # buffer uninitialised for every other graph.
     counters = {}       # device index -> int32 [65536]
     side_counters = {}  # (device index, stream handle) -> int32 [65536]
@@ -432,7 +431,8 @@ def hip_ops() -> SimpleNamespace:
         w4 = cfg == W4_CFG  # four-wave 256 x 256 kernel: N a multiple of 16, offsets below 2 GiB
         _req(0 <= cfg <= W4_CFG and K % 128 == 0 and N % (16 if pp or w4 else bn) == 0 and 1 <= split_k <= K // 128
              and epi in (0, 2) and (not pp or (M * K < 1 << 32 and N * K < 1 << 32))
-             and (not w4 or ((M + 256) * K < 1 << 31 and (N + 256) * K < 1 << 31)),
+             and (not w4 or ((M + 256) * K < 1 << 31 and (N + 256) * K < 1 << 31))
+             and (not (pp or w4) or 2 * (M + 256) * N < 1 << 31),
              f"gemm_nt_fp8: shape {M}x{N}x{K} epi {epi} split {split_k} unsupported by tile {cfg}")
         if out is None:
             out = torch.empty(M, N, dtype=torch.bfloat16, device=xq.device)

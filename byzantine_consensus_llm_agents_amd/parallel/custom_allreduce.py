@@ -114,14 +114,21 @@ class _Rank:
         self.max_blocks = mb.value
         self.calls = {1: 0, 2: 0}
         self.route_max = cap_bytes   # messages routed to the kernels (RCCL above); calibrate() may lower it
+        self.capture_route_max = cap_bytes  # the same inside a HIP-graph capture (decode): >= DECODE_FLOOR
         self.oneshot_limit = None    # measured one-shot limit (None: the choose_mode rule)
         self.addnorm_oneshot_limit = None  # ... of the fused all-reduce + add + RMSNorm kernels
         self.calibration = None
 
     def can(self, x: torch.Tensor) -> bool:
         n = x.numel()
-        return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and n > 0 and n % 8 == 0
-                and 2 * n <= min(self.cap_bytes, self.route_max))
+        if not (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and n > 0 and n % 8 == 0
+                and 2 * n <= self.cap_bytes):
+            return False
+        # eager calls (prefill) follow the measurement; captured calls (decode graphs) stay on the
+        # kernels up to DECODE_FLOOR whatever RCCL measured (an RCCL call inside a captured step
+        # is a path this build does not test)
+        return 2 * n <= self.route_max or (2 * n <= self.capture_route_max
+                                           and torch.cuda.is_current_stream_capturing())
 
     def all_reduce_(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, stream=None,
                     mode: Optional[int] = None) -> torch.Tensor:
@@ -156,18 +163,24 @@ class _Rank:
         the fused all-reduce + add + RMSNorm kernels are timed too, on [nb / 2 / hidden, hidden]
         rows, and their own one-shot limit routes ``all_reduce_add_rmsnorm``.
 
-        Messages up to ``DECODE_FLOOR`` always stay on the kernels whatever RCCL measures: the
-        decode graphs capture these calls, and an RCCL call inside a captured step is a path this
-        build does not test."""
+        Captured messages up to ``DECODE_FLOOR`` stay on the kernels whatever RCCL measures
+        (``capture_route_max``): the decode graphs capture these calls, and an RCCL call inside a
+        captured step is a path this build does not test.  Eager calls follow the measured
+        ``route_max``; both are reported."""
         import torch.distributed as dist
         sizes = sizes or [nb for nb in (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20) if nb <= self.cap_bytes]
         dev = torch.device("cuda", torch.cuda.current_device())
         table = torch.zeros(5, len(sizes), dtype=torch.float64, device=dev)
+        # the fused kernels are timed only where they run at every calibrated size (H <= 8192);
+        # a wider model keeps RCCL / all-reduce + add_rmsnorm (addnorm_oneshot_limit stays None)
+        fused = bool(hidden) and all(
+            self.can_addnorm(torch.empty(max(1, nb // (2 * hidden)), hidden, dtype=torch.bfloat16, device=dev))
+            for nb in sizes)
         for i, nb in enumerate(sizes):
             x = torch.zeros(nb // 2, dtype=torch.bfloat16, device=dev)
             fns = [lambda: self.all_reduce_(x, mode=1), lambda: self.all_reduce_(x, mode=2),
                    lambda: dist.all_reduce(x, group=group)]
-            if hidden:
+            if fused:
                 rows = max(1, nb // (2 * hidden))
                 xa = torch.zeros(rows, hidden, dtype=torch.bfloat16, device=dev)
                 ra, wa = torch.zeros_like(xa), torch.ones(hidden, dtype=torch.bfloat16, device=dev)
@@ -187,15 +200,16 @@ class _Rank:
         dist.all_reduce(table, op=dist.ReduceOp.MAX, group=group)
         t = table.cpu().tolist()
         self.oneshot_limit, route_max = pick_thresholds(sizes, t[0], t[1], t[2], self.cap_bytes)
-        route_max = max(route_max, min(self.cap_bytes, DECODE_FLOOR))
+        capture_route_max = max(route_max, min(self.cap_bytes, DECODE_FLOOR))
         if route:
-            self.route_max = route_max
-        if hidden:
+            self.route_max, self.capture_route_max = route_max, capture_route_max
+        if fused:
             self.addnorm_oneshot_limit = pick_thresholds(sizes, t[3], t[4], t[2], self.cap_bytes)[0]
         self.calls = {1: 0, 2: 0}
         self.calibration = {"sizes": sizes, "oneshot_us": t[0], "twoshot_us": t[1], "rccl_us": t[2],
-                            "oneshot_limit": self.oneshot_limit, "route_max": route_max}
-        if hidden:
+                            "oneshot_limit": self.oneshot_limit, "route_max": route_max,
+                            "capture_route_max": capture_route_max}
+        if fused:
             self.calibration.update(addnorm_oneshot_us=t[3], addnorm_twoshot_us=t[4],
                                     addnorm_oneshot_limit=self.addnorm_oneshot_limit, hidden=hidden)
         return self.calibration

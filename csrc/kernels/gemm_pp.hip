@@ -412,8 +412,9 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
     // bf16: buffer-addressed and 16-B wide, as csrc/kernels/gemm_w4.hip: one v_permlane16_swap
     // per value turns the quads of blocks (2p, 2p+1) into 8 contiguous columns per lane (lane
     // row fq: block 2p + (fq & 1), columns 8 (fq >> 1) ..); rows past M fall outside the
-    // descriptor's range, a column past N gets an out-of-range offset, m-block mb's rows ride in
-    // the SGPR offset.  Half the stores, no per-quad branch.
+    // descriptor's range, a column past N gets an out-of-range offset.  The whole offset rides in
+    // the VGPR: only that part is range-checked (an SGPR offset is added after the check, so a
+    // row past M carried there would be written).  Half the stores, no per-quad branch.
     typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
     typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
     constexpr bool SILU = EPI == EPI_SILU_MUL;
@@ -446,8 +447,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
 #pragma unroll
       for (int e = 0; e < 4; ++e) lo[e] = f2bf(o[e]), hi[e] = f2bf(o[4 + e]);
       const u32x2v l2 = __builtin_bit_cast(u32x2v, lo), h2 = __builtin_bit_cast(u32x2v, hi);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4v{l2[0], l2[1], h2[0], h2[1]}, rc, rowv + colv,
-                                             static_cast<uint32_t>(mb * 16) * ldb, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4v{l2[0], l2[1], h2[0], h2[1]}, rc,
+                                             rowv + colv + static_cast<uint32_t>(mb * 16) * ldb, 0, 0);
     };
     const u32x4v zero = {0, 0, 0, 0};
     if constexpr (SILU) {
@@ -487,8 +488,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(
         if (EPI == EPI_RESIDUAL && mb + 1 < 8) {  // the next m-block's residual in flight
 #pragma unroll
           for (int p = 0; p < 2; ++p)
-            rq[cur ^ 1][p] = __builtin_amdgcn_raw_buffer_load_b128(rr, rowv + colv[p],
-                                                                   static_cast<uint32_t>((mb + 1) * 16) * ldb, 0);
+            rq[cur ^ 1][p] = __builtin_amdgcn_raw_buffer_load_b128(
+                rr, rowv + colv[p] + static_cast<uint32_t>((mb + 1) * 16) * ldb, 0, 0);
         }
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
@@ -567,6 +568,8 @@ BCG_API int bcg_gemm_pp(int epi, const void* x, const void* w, const void* bias,
                         void* ws, void* counters, int M, int N, int K, int inter, int split_k, hipStream_t stream) {
   if (M <= 0 || N <= 0 || N % 16 || K % PBK || K <= 0 || split_k < 1 || K / PBK < split_k) return -2;
   if (2ull * M * K >= (1ull << 32) || 2ull * N * K >= (1ull << 32)) return -2;  // 32-bit buffer offsets
+  // output / residual offsets (a masked column's 0x80000000 bias included) stay 32-bit
+  if (2ull * (M + 256) * (epi == EPI_SILU_MUL ? inter : N) >= (1ull << 31)) return -2;
   if (split_k > 1 && (!ws || !counters)) return -2;
   float* wsf = static_cast<float*>(ws);
   int* cnt = static_cast<int*>(counters);
@@ -591,6 +594,7 @@ BCG_API int bcg_gemm_pp_fp8(int epi, const void* xq, const void* wq, const float
   if (M <= 0 || N <= 0 || N % 16 || K % 128 || K <= 0 || split_k < 1 || K / 128 < split_k) return -2;
   if (!x_scale || !w_scale) return -2;
   if (1ull * M * K >= (1ull << 32) || 1ull * N * K >= (1ull << 32)) return -2;  // 32-bit buffer offsets
+  if (2ull * (M + 256) * N >= (1ull << 31)) return -2;                          // output offsets
   if (split_k > 1 && (!ws || !counters)) return -2;
   float* wsf = static_cast<float*>(ws);
   int* cnt = static_cast<int*>(counters);

@@ -434,8 +434,10 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       // block 2p + (fq & 1), columns 8 (fq >> 1) .. +7 -- half the stores and loads.
       // Offsets are bytes from the item's output corner (C + m0 ldc + its first column): rows
       // past M fall outside the descriptor's range (stores dropped, loads 0), a column past N
-      // gets an offset past every range, m-block j's rows ride in the SGPR offset -- no
-      // per-quad branch, no 64-bit address math.
+      // gets an offset past every range -- no per-quad branch, no 64-bit address math.  The whole
+      // offset (m-block j's rows included) rides in the VGPR: only that part is range-checked (an
+      // SGPR offset is added after the check), and the host bounds (M + 256) * ldc * 2 below
+      // 2^31 so a masked column's 0x80000000 + offset never wraps into range.
       constexpr bool SILU = EPI == EPI_SILU_MUL;
       constexpr int NP = SILU ? NB / 4 : NB / 2;  // 8-column groups per m-block per lane
       constexpr int JG = 1;                       // m-blocks per residual batch
@@ -479,7 +481,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
           *reinterpret_cast<u32x4*>(smem + sbase + (r * CH + (c ^ swz(r))) * 16) = pack8(o);
           return;
         }
-        __builtin_amdgcn_raw_buffer_store_b128(pack8(o), rc, rowv + colv[p], static_cast<uint32_t>(j * MB) * ldb, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(pack8(o), rc, rowv + colv[p] + static_cast<uint32_t>(j * MB) * ldb, 0, 0);
       };
       // the pass of m-blocks j0, j0 + 1 (rows 16 j0 ..): read row-major, store whole rows
       auto flush = [&](int j0) {
@@ -493,8 +495,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         for (int i = 0; i < 32 / RPI; ++i) {
           const int r = i * RPI + lane / LPR;
           const u32x4 v = *reinterpret_cast<const u32x4*>(smem + sbase + (r * CH + (c ^ swz(r))) * 16);
-          __builtin_amdgcn_raw_buffer_store_b128(v, rc, static_cast<uint32_t>(wm * 128 + r) * ldb + cv,
-                                                 static_cast<uint32_t>(j0 * MB) * ldb, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(v, rc, static_cast<uint32_t>(wm * 128 + j0 * MB + r) * ldb + cv, 0, 0);
           if (i & 1) __builtin_amdgcn_sched_barrier(0);  // (two rows of reads in flight, not all)
         }
       };
@@ -532,8 +533,8 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
             for (int jj = 0; jj < JG; ++jj)
 #pragma unroll
               for (int p = 0; p < NP; ++p)
-                rq[bf][jj][p] = __builtin_amdgcn_raw_buffer_load_b128(rr_rs, rowv + colv[p],
-                                                                      static_cast<uint32_t>((j0 + jj) * MB) * ldb, 0);
+                rq[bf][jj][p] = __builtin_amdgcn_raw_buffer_load_b128(
+                    rr_rs, rowv + colv[p] + static_cast<uint32_t>((j0 + jj) * MB) * ldb, 0, 0);
           }
         };
         // one body per bias case (a uniform branch here, not one per quad); the bias groups
@@ -683,8 +684,8 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
             if constexpr (EPI == EPI_RESIDUAL) {
 #pragma unroll
               for (int j = 0; j < NB; ++j)
-                rq[j][pp] = __builtin_amdgcn_raw_buffer_load_b128(rres, rowv + colv[pp],
-                                                                  static_cast<uint32_t>(j * MB) * ldb, 0);
+                rq[j][pp] = __builtin_amdgcn_raw_buffer_load_b128(
+                    rres, rowv + colv[pp] + static_cast<uint32_t>(j * MB) * ldb, 0, 0);
             }
           }
 #pragma unroll
@@ -712,8 +713,8 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
               }
               const u32x2 lo = __builtin_bit_cast(u32x2, pack4(o[0], o[1], o[2], o[3]));
               const u32x2 hi = __builtin_bit_cast(u32x2, pack4(o[4], o[5], o[6], o[7]));
-              __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo[0], lo[1], hi[0], hi[1]}, rc, rowv + colv[pp],
-                                                     static_cast<uint32_t>(j * MB) * ldb, 0);
+              __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo[0], lo[1], hi[0], hi[1]}, rc,
+                                                     rowv + colv[pp] + static_cast<uint32_t>(j * MB) * ldb, 0, 0);
             }
           }
           __builtin_amdgcn_sched_barrier(0);
@@ -1013,6 +1014,8 @@ BCG_API int bcg_gemm_w4(int epi, const void* x, const void* w, const void* bias,
   if (M <= 0 || N <= 0 || N % 16 || K % BK || K <= 0 || split_k < 1 || K / BK < split_k) return -2;
   // 32-bit buffer offsets, rows up to a whole tile past the end included
   if (2ull * (M + BM) * K >= (1ull << 31) || 2ull * (N + BN) * K >= (1ull << 31)) return -2;
+  // the output (and residual) offsets, a masked column's 0x80000000 bias included, stay 32-bit
+  if (2ull * (M + BM) * (epi == EPI_SILU_MUL ? inter : N) >= (1ull << 31)) return -2;
   if (split_k > 1 && (!ws || !counters)) return -2;
   float* wsf = static_cast<float*>(ws);
   int* cnt = static_cast<int*>(counters);
@@ -1037,6 +1040,7 @@ BCG_API int bcg_gemm_w4_fp8(int epi, const void* xq, const void* wq, const float
   if (M <= 0 || N <= 0 || N % 16 || K % 128 || K <= 0 || split_k < 1 || K / 128 < split_k) return -2;
   if (!x_scale || !w_scale) return -2;
   if (1ull * (M + BM) * K >= (1ull << 31) || 1ull * (N + BN) * K >= (1ull << 31)) return -2;
+  if (2ull * (M + BM) * N >= (1ull << 31)) return -2;  // 32-bit output offsets (see bcg_gemm_w4)
   if (split_k > 1 && (!ws || !counters)) return -2;
   float* wsf = static_cast<float*>(ws);
   int* cnt = static_cast<int*>(counters);

@@ -21,10 +21,10 @@ KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "
         "scaling", "vs_baseline", "dtype", "data", "config"}
 
 
-def _run(extra, timeout=300):
+def _run(extra, timeout=300, env_extra=None):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--backend", "fake", "--sims-per-gpu", "2",
            "--honest", "4", "--byzantine", "1", "--window-s", "1"] + extra
-    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env = dict(os.environ, OMP_NUM_THREADS="1", **(env_extra or {}))
     env.pop("WORLD_SIZE", None)
     p = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=timeout)
     assert p.returncode == 0, p.stderr[-3000:]
@@ -109,3 +109,45 @@ def test_bench_hostmodel_backend_reports_host_budget():
     h = out["detail"]["host"]
     assert out["detail"]["decisions"] > 0 and h["cpu_s_per_decision"] > 0
     assert h["min_replica_decisions_per_s"] > 0 and out["detail"]["tokens_per_s"] > 0
+
+
+def test_bench_reports_retry_overhead_with_fault_injector():
+    """the timed region's retry-ladder cost is in detail.retry.  agent_1's
+    decide requests always fail (unparsable JSON): every one of its decisions goes through the
+    batch retry, the sequential 3-attempt loop, and exhausts."""
+    rules = [{"agent": "agent_1", "round": r, "phase": "decide", "tries": "all", "mode": "invalid_json"}
+             for r in range(1, 5)]
+    out = _run(["--steps", "3", "--warmup", "1", "--age-p", "0", "--max-rounds", "4"],
+               env_extra={"BCG_FAKE_FAULTS": json.dumps(rules)})
+    r = out["detail"]["retry"]
+    assert r["decide_prompts"] > 0 and r["vote_prompts"] > 0
+    assert r["decisions_exhausted"] > 0 and r["sequential_calls"] > 0
+    assert r["sequential_attempts"] >= 3 * r["decisions_exhausted"] - 3  # (a window may cut a loop)
+    assert r["retry_rows"] > 0 and r["engine_rows_per_prompt"] > 1.0
+    host = out["detail"]["host"]
+    assert host["threads_per_rank"] >= 2 and "cpu_s_by_thread_rank0" in host
+
+
+def test_bench_retry_counters_zero_without_faults():
+    out = _run(["--steps", "2", "--warmup", "1", "--age-p", "0"])
+    r = out["detail"]["retry"]
+    assert r["decisions_exhausted"] == 0 and r["votes_exhausted"] == 0 and r["retry_rows"] >= 0
+
+
+@pytest.mark.parametrize("tp,parallelism", [(4, "dp2xtp4"), (2, "dp4xtp2")])
+def test_bench_world8_layouts(tp, parallelism):
+    """the BASELINE layouts of configs 4 (TP=4 x DP=2) and 5 (TP=2 x DP=4) at
+    world 8 (gloo ranks, scripted engine): one JSON line, one game pool per replica (its group's
+    driver) with its own seeds, followers run no games, decisions summed over replicas only."""
+    out = _run(["--gpus", "8", "--tp", str(tp), "--steps", "2", "--warmup", "1"], timeout=600)
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == parallelism
+    replicas = 8 // tp
+    assert out["config"]["global_batch"] == 2 * 5 * replicas
+    ranks = sorted(out["detail"]["ranks"], key=lambda r: r["rank"])
+    assert [r["rank"] for r in ranks] == list(range(8))
+    assert [r["replica"] for r in ranks] == [i // tp for i in range(8)]
+    drivers = [r for r in ranks if r["driver"]]
+    assert [r["rank"] for r in drivers] == [tp * k for k in range(replicas)]
+    assert len({r["seed_base"] for r in drivers}) == replicas and all(r["sims"] == 2 for r in drivers)
+    assert all(r["decisions"] == 0 and r["sims"] == 0 for r in ranks if not r["driver"])
+    assert out["detail"]["decisions"] == sum(r["decisions"] for r in drivers) > 0

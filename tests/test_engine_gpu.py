@@ -83,16 +83,14 @@ def test_llm_guided_json_all_schemas():
     assert eng.graphs is not None and eng.graphs.captures >= 1
 
 
-def test_continuous_batching_overlapped_prefill():
-    """Async engine thread + prefill stream: clients arrive while earlier rows decode."""
+def test_continuous_batching_async_clients():
+    """Async engine thread: clients arrive while earlier rows decode."""
     import threading
     from byzantine_consensus_llm_agents_amd.bcg import prompts as P
     from byzantine_consensus_llm_agents_amd.bcg.config import ENGINE_CONFIG
     from byzantine_consensus_llm_agents_amd.engine import GuidedDecodingParams, LLM, SamplingParams
     ENGINE_CONFIG["budget_aware_json"] = True
-    llm = LLM("bcg/tiny-qwen3", backend="hip", seed=9, max_model_len=4096, kv_cache_gb=2.0,
-              overlap_prefill=True)
-    assert llm.backend.overlap
+    llm = LLM("bcg/tiny-qwen3", backend="hip", seed=9, max_model_len=4096, kv_cache_gb=2.0)
     llm.start_continuous_batching()
     schemas = [P.honest_decision_schema(0, 50), P.vote_schema(P.HONEST_VOTE_OPTIONS)]
     results, errors = {}, []

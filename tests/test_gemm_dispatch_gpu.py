@@ -44,10 +44,10 @@ def hip():
     from byzantine_consensus_llm_agents_amd.ops import get_ops
     ops = get_ops("hip")
     plan = ops.gemm_plan
-    saved = (plan.mode, plan.avoid_library, plan.force_split)
-    plan.mode, plan.avoid_library, plan.force_split = "1", False, 1  # the shipped table
+    saved = (plan.mode, plan.force_split)
+    plan.mode, plan.force_split = "1", 1  # the shipped table
     yield ops
-    plan.mode, plan.avoid_library, plan.force_split = saved
+    plan.mode, plan.force_split = saved
 
 
 def _err(out, ref):

@@ -251,3 +251,50 @@ def test_gemm_pp_fp8(hip, M, N, K, split, epi, cfg):
             want = ref + b.float()
             got = hip.gemm_nt_fp8(xq, xs, wq, ws, (cfg, split), 0, bias=b)
         _close(got, want)
+
+
+@pytest.mark.parametrize("cfg", [10, 11])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+@pytest.mark.parametrize("M", [37, 257])
+def test_gemm_big_tile_partial_m_leaves_rows_past_m(hip, cfg, epi, M):
+    """A partial last M tile of the 256x256 kernels must not touch rows >= M: the output (and
+    residual) are views buf[:M] of a larger buffer whose extra rows hold a sentinel."""
+    torch.manual_seed(M + epi)
+    N, K = 512, 1024
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
+    width = N // 2 if epi == 1 else N
+    buf = torch.full((M + 256, width), 7.0, device="cuda", dtype=torch.bfloat16)
+    out = buf[:M]
+    ref = _ref(x, w)
+    if epi == 1:
+        ref = torch.nn.functional.silu(ref[:, :width]) * ref[:, width:]
+    res = None
+    if epi == 2:
+        rbuf = torch.full((M + 256, N), -3.0, device="cuda", dtype=torch.bfloat16)
+        rbuf[:M] = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+        res = rbuf[:M]
+        ref = ref + res.float()
+    got = hip.gemm_nt(x, w, cfg, epi, residual=res, out=out)
+    _close(got, ref)
+    assert torch.all(buf[M:] == 7.0), "rows past M were written"
+    if epi == 2:
+        assert torch.all(rbuf[M:] == -3.0)
+
+
+@pytest.mark.parametrize("cfg", [10, 11])
+@pytest.mark.parametrize("epi", [0, 2])
+@pytest.mark.parametrize("M", [37, 257])
+def test_gemm_fp8_big_tile_partial_m_leaves_rows_past_m(hip, cfg, epi, M):
+    N, K = 512, 1024
+    xq, xs, wq, ws, ref = _fp8_operands(M, N, K, 3 * M + epi)
+    buf = torch.full((M + 256, N), 7.0, device="cuda", dtype=torch.bfloat16)
+    res = None
+    if epi == 2:
+        res = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+        buf[:M] = res
+        ref = ref + res.float()
+        res = buf[:M]
+    got = hip.gemm_nt_fp8(xq, xs, wq, ws, cfg, epi, residual=res, out=buf[:M])
+    _close(got, ref)
+    assert torch.all(buf[M:] == 7.0), "rows past M were written"

@@ -33,19 +33,6 @@ def test_pp_shape_rules(monkeypatch):
     assert not p.supported(PP_CFG, 64, 256, 100, 0)        # K % 64
 
 
-def test_avoid_library_picks_fastest_hand_config(tmp_path, monkeypatch):
-    """Overlapped prefill: a shape whose table entry is the library must still get a hand kernel
-    (the fastest measured hand configuration, else the 256x256 kernel)."""
-    monkeypatch.setenv("BCG_HAND_GEMM", "1")
-    p = _plan(tmp_path, {"768,34816,5120,1": [-1, 1]},
-              {"768,34816,5120,1": {"lib": 290.0, "8x1": 345.0, "10x1": 300.0, "7x1": 350.0}})
-    assert p.choose(768, 34816, 5120, 1) is None
-    p.avoid_library = True
-    assert p.choose(768, 34816, 5120, 1) == (10, 1)
-    assert p.choose(16384, 5120, 17408, 2) == (PP_CFG, 1)  # unmeasured: the 256x256 kernel
-    assert p.choose(5, 4096, 4096, 0) is not None
-
-
 def test_fp8_plan_table_rule_and_library(tmp_path, monkeypatch):
     """fp8 projections: measured shapes follow the table (nearest M above, library beyond the
     largest measured M or where it won), unmeasured shapes the hand kernel up to M = 128."""
