@@ -98,6 +98,10 @@ ENGINE_CONFIG = {
     # only while >= admit_min_live rows decode.  3 vs 0, two A/B pairs on one GPU: 31.0k / 31.5k
     # vs 30.6k / 30.8k tokens/s (profiles/bench_r2_ab*_a*.json)
     "admit_max_wait": int(os.environ.get("BCG_ADMIT_MAX_WAIT", "3")),
+    # run only full prefill chunks while the decode batch is fed: a wave's partial last chunk
+    # waits (its prompts pending with their KV so far) up to this many more bursts for the
+    # next wave (engine.py `_hold_tail`); 0 = run it at once
+    "prefill_carry_bursts": int(os.environ.get("BCG_PREFILL_CARRY", "0")),
     # tests only: run the model with this many decoder layers (real layer shapes, reduced depth)
     "num_layers_override": None,
 }

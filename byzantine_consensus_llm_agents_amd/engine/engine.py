@@ -95,6 +95,10 @@ class EngineArgs:
     admit_max_wait: int = 0
     admit_min_live: int = 64
     admit_min_tokens_frac: float = 1.5
+    # full prefill chunks only while the decode batch is fed: the last, partial chunk of a wave
+    # is carried (its prompts stay pending with their KV so far) into the next wave, for at most
+    # this many more bursts; 0 = every wave runs its tail chunk at once
+    prefill_carry_bursts: int = 0
     # decode attention reads KV blocks shared by several rows (prefix cache) once per group
     # of rows instead of once per row (engine/cascade.py); HIP backend only
     cascade_decode: bool = True
@@ -125,6 +129,7 @@ class EngineArgs:
                    precapture_graphs=ec.get("precapture_graphs", True),
                    kv_cache_dtype=ec.get("kv_cache_dtype", "auto"),
                    admit_max_wait=int(ec.get("admit_max_wait", 0)),
+                   prefill_carry_bursts=int(ec.get("prefill_carry_bursts", 0)),
                    cascade_decode=bool(ec.get("cascade_decode", True)))
         dtype = ec.get("dtype", "bfloat16")
         args.dtype = getattr(torch, dtype) if isinstance(dtype, str) else dtype
@@ -144,6 +149,7 @@ class _Seq:
     fsm_base: int = -1              # device row base, assigned by the scheduler thread
     blocks: List[int] = field(default_factory=list)
     cached: int = 0
+    done_pos: int = 0               # prompt tokens whose KV is written (prefix cache + prefilled chunks)
     error: Optional[str] = None
 
 
@@ -152,7 +158,9 @@ class InferenceEngine:
         self.args = args
         self.timer = PhaseTimer()
         self.stats = {"prompt_tokens": 0, "cached_tokens": 0, "generated_tokens": 0,
-                      "decode_steps": 0, "decode_row_steps": 0, "prefill_chunks": 0, "calls": 0}
+                      "decode_steps": 0, "decode_row_steps": 0, "prefill_chunks": 0, "prefill_full_chunks": 0,
+                      "prefill_tail_tokens": 0, "prefill_carried": 0, "calls": 0}
+        self._carry: List["_Request"] = []  # admitted, prefill incomplete (pending), oldest first
         cfg = args.model_cfg
         self.backend = args.backend
         if self.backend == "hip" and not torch.cuda.is_available():
@@ -449,6 +457,7 @@ class InferenceEngine:
 
     def _fail_all(self, exc):
         self._snap = None
+        self._carry = []  # (their slots are failed below)
         with self._cv:
             pending = list(self._incoming) + list(self._waiting)
             self._incoming.clear()
@@ -612,44 +621,75 @@ class InferenceEngine:
         if self._bursts - self._waiting[0].enq_burst >= a.admit_max_wait:
             return False
         queued = sum(len(r.seq.prompt_ids) for r in self._waiting)
+        queued += sum(len(r.seq.prompt_ids) - r.seq.done_pos for r in self._carry)
         return queued < a.admit_min_tokens_frac * a.prefill_chunk_tokens
 
-    def _admit(self):
-        with self._cv:
-            if not self._waiting:
-                return
-            if self._admission_deferred():
-                return
-            free = [i for i, r in enumerate(self.slots) if r is None]
-            cap = self.args.max_batch_seqs
-            if self.args.honor_max_num_seqs and self.args.max_num_seqs:
-                cap = min(cap, self.args.max_num_seqs)
-            budget = max(0, cap - (len(self.slots) - len(free)))
-            admitted = []
-            while self._waiting and free and len(admitted) < budget:
-                req = self._waiting[0]
-                a = self.blocks.allocate(req.seq.prompt_ids, req.seq.max_new, self.args.prefix_caching)
-                if not a.ok:
-                    break
-                self._waiting.popleft()
-                req.seq.blocks, req.seq.cached = list(a.blocks), a.num_cached_tokens
-                req.row = free.pop(0)
-                req.pending = True
-                self.slots[req.row] = req
-                admitted.append(req)
-            if not admitted and not any(self.slots) and self._waiting:
-                raise RuntimeError("KV cache too small for a single waiting sequence")
-        if admitted:
-            self._prefill(admitted)
+    def _hold_tail(self) -> bool:
+        """Carry this wave's partial last chunk to the next wave (deterministic under TP: live
+        rows and burst counts only): the decode batch is fed and no carried prompt has waited
+        past its budget."""
+        a = self.args
+        if a.prefill_carry_bursts <= 0:
+            return False
+        live = sum(1 for r in self.slots if r is not None and not r.pending)
+        if live < a.admit_min_live:
+            return False
+        oldest = min((r.enq_burst for r in self._carry), default=self._bursts)
+        return self._bursts - oldest < a.admit_max_wait + a.prefill_carry_bursts
 
-    def _prefill(self, reqs: List["_Request"]):
-        """Prefill the admitted prompts, then activate them: write their state rows, commit the
-        prompt blocks, sample token 1."""
-        seqs = [r.seq for r in reqs]
+    def _admit(self):
+        admitted = []
+        with self._cv:
+            if self._waiting and not self._admission_deferred():
+                admitted = self._admit_locked()
+        wave, self._carry = self._carry + admitted, []
+        if wave and (admitted or not self._hold_tail()):
+            self._prefill(wave)
+        else:
+            self._carry = wave
+
+    def _admit_locked(self) -> List["_Request"]:
+        free = [i for i, r in enumerate(self.slots) if r is None]
+        cap = self.args.max_batch_seqs
+        if self.args.honor_max_num_seqs and self.args.max_num_seqs:
+            cap = min(cap, self.args.max_num_seqs)
+        budget = max(0, cap - (len(self.slots) - len(free)))
+        admitted = []
+        while self._waiting and free and len(admitted) < budget:
+            req = self._waiting[0]
+            a = self.blocks.allocate(req.seq.prompt_ids, req.seq.max_new, self.args.prefix_caching)
+            if not a.ok:
+                break
+            self._waiting.popleft()
+            req.seq.blocks, req.seq.cached = list(a.blocks), a.num_cached_tokens
+            req.seq.done_pos = a.num_cached_tokens
+            req.row = free.pop(0)
+            req.pending = True
+            self.slots[req.row] = req
+            admitted.append(req)
+        if not admitted and not any(self.slots) and self._waiting:
+            raise RuntimeError("KV cache too small for a single waiting sequence")
+        return admitted
+
+    def _prefill(self, wave: List["_Request"]):
+        """Prefill the wave's uncached prompt tokens; prompts whose prompt is complete are then
+        activated (state rows, prompt blocks committed, token 1 sampled), the others -- their
+        tokens in a held partial chunk -- stay pending in the carry."""
+        seqs = [r.seq for r in wave]
         table_cpu = self._block_table(seqs, len(seqs))
         with self.timer.phase("prefill"):
-            plans = self._plan_prefill(seqs, table_cpu)
+            plans = self._plan_prefill(seqs, table_cpu, hold_tail=self._hold_tail())
             logits = self._run_prefill(plans, len(seqs))
+        done = [i for i, s in enumerate(seqs) if s.done_pos == len(s.prompt_ids)]
+        self._carry = [r for r, s in zip(wave, seqs) if s.done_pos < len(s.prompt_ids)]
+        self.stats["prefill_carried"] += len(self._carry)
+        if not done:
+            return
+        if len(done) < len(wave):
+            logits = logits.index_select(0, self._h2d(torch.tensor(done, dtype=torch.long)))
+        reqs = [wave[i] for i in done]
+        seqs = [r.seq for r in reqs]
+        table_cpu = table_cpu[done]
         st = self.state
         rows_d = self._h2d(torch.tensor([r.row for r in reqs], dtype=torch.long))
         st["block_tables"].index_copy_(0, rows_d, self._h2d(table_cpu))
@@ -796,15 +836,18 @@ class InferenceEngine:
             return t
         return t.pin_memory().to(self.device, non_blocking=True)
 
-    def _plan_prefill(self, wave: List[_Seq], table_cpu: torch.Tensor) -> List[tuple]:
-        """Pack the uncached prompt tokens into chunks of exactly `prefill_chunk_tokens`
+    def _plan_prefill(self, wave: List[_Seq], table_cpu: torch.Tensor, hold_tail: bool = False) -> List[tuple]:
+        """Pack the not-yet-prefilled prompt tokens into chunks of exactly `prefill_chunk_tokens`
         (a prompt may straddle chunks; only the last chunk is shorter), so the
-        prefill GEMMs run at one M that the shipped TunableOp table covers.
-        Every chunk's metadata is uploaded before any forward is launched."""
+        prefill GEMMs run at one M that the shipped tables cover -- M = 16384 is also the one M
+        where every projection's 256 x 256 tiles split evenly over 256 CUs.  `hold_tail`: the
+        partial last chunk is not run (its prompts keep `done_pos` where it starts).
+        Advances each sequence's `done_pos`.  Every chunk's metadata is uploaded before any
+        forward is launched."""
         budget = self.args.prefill_chunk_tokens
         plans, chunk, used = [], [], 0
         for r, s in enumerate(wave):
-            pos, n = s.cached, len(s.prompt_ids)
+            pos, n = s.done_pos, len(s.prompt_ids)
             while pos < n:
                 take = min(n - pos, budget - used)
                 chunk.append((r, pos, pos + take))
@@ -812,9 +855,15 @@ class InferenceEngine:
                 pos += take
                 if used == budget:
                     plans.append(self._plan_chunk(wave, chunk, table_cpu))
+                    for rr, _, b in chunk:
+                        wave[rr].done_pos = b
                     chunk, used = [], 0
-        if chunk:
+        if chunk and not hold_tail:
             plans.append(self._plan_chunk(wave, chunk, table_cpu))
+            for rr, _, b in chunk:
+                wave[rr].done_pos = b
+            self.stats["prefill_tail_tokens"] += used
+        self.stats["prefill_full_chunks"] += len(plans) - (1 if chunk and not hold_tail else 0)
         return plans
 
     def _plan_chunk(self, wave, chunk, table_cpu):

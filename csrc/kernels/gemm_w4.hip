@@ -924,11 +924,16 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
 
   // ---- split-K (one item per workgroup): every split stores its fp32 tile write-through (sc1);
-  // the last arriver sums all the slabs (its own included) straight into the epilogue -- the
-  // accumulators die at the store, so the reduction needs no second register copy of the tile.
-  // Slab layout: per (wave, block, 16-B quarter) 256 floats, lane-major (any layout both sides
-  // agree on).
+  // the last arriver adds the OTHER splits' slabs into its own accumulators and runs the
+  // ordinary epilogue.  The slabs come in by LDS-DMA, 16 KiB per wave per round into two
+  // alternating LDS buffers (a round in flight while the previous one is added): many loads in
+  // flight and no VGPRs held for them.  (Summing through per-block register loads inside the
+  // epilogue put ~190 dependent round trips on one CU: ~70 us of a 105-us qkv launch at 704
+  // rows, profiles/r5_gemm_feed.)  Slab layout: per (wave, block, 16-B quarter) 256 floats,
+  // lane-major, so a wave's 64 pieces are one contiguous 64 KiB and a piece lands lane-linearly
+  // exactly where that lane reads it back.
   constexpr int QPB = L32 ? 4 : 1;  // 16-B quarters per block per lane
+  static_assert(NB * NB * QPB == 64, "64 pieces of 1 KiB per wave and slab");
   float* slab = ws + static_cast<size_t>(gc.tile) * split_k * (BM * BN);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, split_k * BM * BN * 4, 0x00020000);
   __syncthreads();  // every wave is past its last ds_read: smem is reusable as the flag slot
@@ -955,20 +960,78 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     flag[0] = last;
   }
   __syncthreads();
-  if (!flag[0]) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  epilogue(gc, [&](int i, int j) {
-    std::remove_reference_t<decltype(acc[0][0])> sum = 0.f;
-    for (int sp = 0; sp < split_k; ++sp)
+  const int is_last = flag[0];
+  __syncthreads();  // every wave has read the flag before the slab rounds overwrite it
+  if (!is_last) return;
+  if constexpr (L32) {  // fp8 / 32x32 layout: per-block register loads (its heavier epilogue has
+                        // no VGPRs to spare for the round scheme's addressing)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    epilogue(gc, [&](int i, int j) {
+      std::remove_reference_t<decltype(acc[0][0])> sum = 0.f;
+      for (int sp = 0; sp < split_k; ++sp)
 #pragma unroll
-      for (int qq = 0; qq < QPB; ++qq) {
-        const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, slab_off(sp, i, j, qq), 0,
-                                                                                        16 /*sc1*/));
+        for (int qq = 0; qq < QPB; ++qq) {
+          const f32x4 v = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, slab_off(sp, i, j, qq), 0, 16 /*sc1*/));
 #pragma unroll
-        for (int e = 0; e < 4; ++e) sum[4 * qq + e] += v[e];
+          for (int e = 0; e < 4; ++e) sum[4 * qq + e] += v[e];
+        }
+      return sum;
+    });
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (and every slab load is sc1)
+  const i32x4 srd = make_srd(slab, static_cast<uint32_t>(split_k) * BM * BN * 4);
+  const uint32_t lds_w = lds_base + static_cast<uint32_t>(wave) * 16384;
+  // round = 16 pieces (f = 16 g ..) of split sp into buffer b (2 x 64 KiB: 4 waves x 16 KiB)
+  auto issue = [&](int sp, int g, int b) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const uint32_t soff = __builtin_amdgcn_readfirstlane(
+          static_cast<uint32_t>(sp) * (BM * BN * 4) + static_cast<uint32_t>(wave * 64 + 16 * g + q) * 1024);
+      const uint32_t m0v = __builtin_amdgcn_readfirstlane(lds_w + b * 65536 + q * 1024);
+      asm volatile("s_mov_b32 m0, %3\n\tbuffer_load_dwordx4 %0, %1, %2 offen sc1 lds"
+                   :
+                   : "v"(static_cast<uint32_t>(lane) * 16), "s"(srd), "s"(soff), "s"(m0v)
+                   : "memory", "m0");
+    }
+  };
+  auto consume = [&](int g, int b) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int f = 16 * g + q, i = f / (NB * QPB), j = (f / QPB) % NB, qq = f % QPB;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(smem + wave * 16384 + b * 65536 + q * 1024 + lane * 16);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float a;
+        asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(a) : "a"(acc[i][j][4 * qq + e]));
+        a += v[e];
+        asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(acc[i][j][4 * qq + e]) : "v"(a));
       }
-    return sum;
-  });
+    }
+    // these reads are done before the round after next refills buffer b
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  const int first = gc.split == 0 ? 1 : 0;  // the other splits, in order
+  if (first < split_k) issue(first, 0, 0);
+  for (int sp = first; sp < split_k; sp = (sp + 1 == gc.split ? sp + 2 : sp + 1)) {
+    const int nsp = sp + 1 == gc.split ? sp + 2 : sp + 1;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {  // (4 rounds per split: the buffer index g & 1 is static)
+      if (g < 3)
+        issue(sp, g + 1, (g + 1) & 1);
+      else if (nsp < split_k)
+        issue(nsp, 0, 0);
+      const bool more = g < 3 || nsp < split_k;
+      if (more)
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // this round landed, the next in flight
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      consume(g, g & 1);
+    }
+  }
+  asm volatile("s_nop 4" ::: "memory");  // (AGPR writes -> the epilogue's reads)
+  epilogue(gc, [&](int i, int j) { return read_acc(acc[i][j]); });
 }
 
 // compute units of the current device (one resident workgroup each: 160 KiB of LDS)

@@ -179,3 +179,46 @@ def test_decode_buckets_cover_every_batch_size():
             assert b - n < 32
         elif n > 1024:
             assert b - n < 64
+
+
+def test_prefill_carry_matches_reference(fresh_engine_state):
+    """Carry-over chunked prefill (prefill_carry_bursts > 0): while rows decode, a wave's
+    partial last chunk is held and its prompts finish in a later wave.  Greedy outputs equal
+    those of an engine that runs every tail chunk at once, and every request completes."""
+    import threading
+    from byzantine_consensus_llm_agents_amd.bcg import prompts as P
+    from byzantine_consensus_llm_agents_amd.engine import GuidedDecodingParams, LLM, SamplingParams
+    schema = P.honest_decision_schema(0, 50)
+    prompts = {(k, rnd): f"<|im_start|>system\nagent {k} " + "history line. " * (3 + 2 * k + rnd)
+               + f"<|im_end|>\n<|im_start|>user\nround {rnd}<|im_end|>\n<|im_start|>assistant\n"
+               for k in range(6) for rnd in range(3)}
+    params = SamplingParams(temperature=0.0, max_tokens=40, guided_decoding=GuidedDecodingParams(json=schema))
+
+    def run(carry):
+        llm = LLM("bcg/tiny-qwen3", backend="torch", seed=5, max_model_len=1024, kv_cache_gb=0.05,
+                  max_batch_seqs=16, budget_aware_json=True, admit_max_wait=0, admit_min_live=1,
+                  prefill_chunk_tokens=96, prefill_carry_bursts=carry, prefix_caching=False)
+        llm.start_continuous_batching()
+        out, errors = {}, []
+
+        def client(k):
+            try:
+                for rnd in range(3):
+                    out[(k, rnd)] = llm.generate([prompts[(k, rnd)]], [params])[0].outputs[0].text
+            except BaseException as exc:
+                errors.append(exc)
+
+        threads = [threading.Thread(target=client, args=(k,)) for k in range(6)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=300)
+        stats = dict(llm.backend.stats)
+        llm.shutdown()
+        assert not errors, errors[0]
+        return out, stats
+
+    ref, _ = run(0)
+    got, stats = run(4)
+    assert len(got) == 18 and got == ref
+    assert stats["prefill_carried"] > 0 and stats["prefill_full_chunks"] > 0
