@@ -32,7 +32,11 @@ engines; ``--tp > 1`` groups consecutive ranks into one tensor-parallel engine
 Data: random-init weights of the real architecture and the synthetic
 byte-level BPE tokenizer (no network for checkpoints); the budget-aware JSON
 grammar guarantees schema-valid outputs from untrained weights at the full
-max_tokens (300 decide / 200 vote) -- a pessimistic decode length.
+max_tokens (300 decide / 200 vote) -- a pessimistic decode length -- and its
+validity-aware form (every property emitted, >= 10 visible characters per
+free-text field) makes them pass the simulator's validity rules, as a trained
+model's outputs do; ``--plain-grammar`` drops that (a random model then sends
+~30 % of its outputs down the retry ladder: ``detail.retry``).
 
 Deadline guard: if the run would pass ``--deadline-s`` (from process start),
 the timed loop stops early and the JSON line reports the windows actually
@@ -55,6 +59,10 @@ sys.path.insert(0, ROOT)
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 BASELINE_VALUE = None  # the reference publishes no number
+# the bench grammar's visible-character floor of free-text fields (engine validity_aware_json):
+# the simulator's validity rules (strategy >= 3, reasoning >= 10 stripped chars) then hold for
+# the random model's outputs, as they do for a trained model's
+VALIDITY_MIN_VISIBLE = 10
 
 
 def parse(argv=None):
@@ -92,6 +100,9 @@ def parse(argv=None):
                     help="fp8 halves KV bytes (reduced precision: never used for the bf16 headline)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
+    ap.add_argument("--plain-grammar", action="store_true",
+                    help="the reference's schemas as given (no validity-aware bench grammar): a random model "
+                         "then closes strings early / skips optional fields and ~30 %% of its outputs retry")
     ap.add_argument("--no-custom-allreduce", action="store_true",
                     help="TP collectives through RCCL only (no xGMI one-/two-shot kernels)")
     ap.add_argument("--kv-cache-gb", type=float, default=None,
@@ -416,6 +427,7 @@ def main(argv=None):
     C.VLLM_CONFIG["tensor_parallel_size"] = args.tp
     C.VLLM_CONFIG["quantization"] = args.quantization
     C.ENGINE_CONFIG.update(backend=args.backend, budget_aware_json=True, seed=args.seed + replica,
+                           validity_aware_json=0 if args.plain_grammar else VALIDITY_MIN_VISIBLE,
                            use_hip_graphs=not args.no_graphs, prefix_caching=not args.no_prefix_cache,
                            custom_allreduce=not args.no_custom_allreduce,
                            kv_cache_dtype=args.kv_cache_dtype)
@@ -592,7 +604,9 @@ def main(argv=None):
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": "fp8" if args.quantization == "fp8" else "bf16",
             "kv_cache_dtype": "fp8" if args.kv_cache_dtype == "fp8" else "bf16",
-            "data": "synthetic (random-init weights, synthetic BPE tokenizer, budget-aware JSON grammar)",
+            "data": "synthetic (random-init weights, synthetic BPE tokenizer, budget-aware JSON grammar"
+                    + ("" if args.plain_grammar else f", validity-aware: every field, >= {VALIDITY_MIN_VISIBLE} "
+                       "visible chars per free-text field") + ")",
             "config": {"model": model, "honest": args.honest, "byzantine": args.byzantine,
                        "global_batch": args.sims_per_gpu * (args.honest + args.byzantine) * (world // args.tp),
                        "sims_per_gpu": args.sims_per_gpu, "seq_len": C.VLLM_CONFIG["max_model_len"],
@@ -603,6 +617,8 @@ def main(argv=None):
                        "step": f"{args.window_s:g} s window of the continuously-batched pool",
                        "parallelism": f"dp{world // args.tp}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
                        "hip_graphs": not args.no_graphs, "prefix_caching": not args.no_prefix_cache,
+                       "grammar": "budget-aware" + ("" if args.plain_grammar else
+                                                    f" + validity-aware({VALIDITY_MIN_VISIBLE})"),
                        "custom_allreduce": args.tp > 1 and not args.no_custom_allreduce},
             "detail": {"decisions": total_decisions, "elapsed_s": round(elapsed, 3), "init_s": round(init_s, 1),
                        "steps_requested": args.steps, "window_s": args.window_s,

@@ -86,6 +86,10 @@ ENGINE_CONFIG = {
     "kv_block_size": 16,
     "seed": None,                  # None = unseeded (reference behaviour)
     "budget_aware_json": False,    # force closing JSON before max_tokens
+    # benchmark grammar for untrained weights: every property emitted, free-text fields with at
+    # least this many visible characters (the simulator's validity rules then hold, as for a
+    # trained model's outputs); 0 = the reference's schemas as given
+    "validity_aware_json": 0,
     "max_whitespace": 4,           # JSON grammar: max consecutive whitespace chars
     "prefix_caching": True,
     "use_hip_graphs": True,

@@ -79,6 +79,9 @@ class EngineArgs:
     max_batch_seqs: int = 512
     prefill_chunk_tokens: int = 16384
     budget_aware_json: bool = False
+    # benchmark grammar for untrained weights: every property emitted, free-text strings with
+    # >= this many visible characters (guided/json_schema.py validity_aware); 0 = the schema as given
+    validity_aware_json: int = 0
     max_whitespace: int = 4
     prefix_caching: bool = True
     use_hip_graphs: bool = True
@@ -121,6 +124,7 @@ class EngineArgs:
                    max_batch_seqs=ec.get("max_batch_seqs", 512),
                    prefill_chunk_tokens=ec.get("prefill_chunk_tokens", 16384),
                    budget_aware_json=ec.get("budget_aware_json", False),
+                   validity_aware_json=int(ec.get("validity_aware_json", 0)),
                    max_whitespace=ec.get("max_whitespace", 4),
                    prefix_caching=ec.get("prefix_caching", True),
                    use_hip_graphs=ec.get("use_hip_graphs", True),
@@ -196,7 +200,7 @@ class InferenceEngine:
         self._req_counter = 0
 
         self.fsm = FSMRegistry(self.tokenizer.all_token_bytes(), cfg.vocab_size, self.device,
-                               max_ws=args.max_whitespace)
+                               max_ws=args.max_whitespace, validity_aware_min=args.validity_aware_json)
         self.eos_ids = (self.tokenizer.eos_token_ids + [self.tokenizer.eos_token_ids[0]])[:2]
         self.n_text_tokens = min(self.tokenizer.vocab_size, cfg.vocab_size)
         self._alloc_kv_cache()

@@ -17,7 +17,7 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
-from .json_schema import schema_to_dfa
+from .json_schema import schema_to_dfa, validity_aware
 
 
 @dataclass
@@ -93,8 +93,10 @@ class FSMRegistry:
     """
 
     def __init__(self, token_bytes: List[bytes], vocab_rows: int, device, max_ws: int = 4,
-                 native: bool = True):
+                 native: bool = True, validity_aware_min: int = 0):
         self.token_bytes = token_bytes
+        # > 0: every schema is compiled in its validity-aware form (json_schema.validity_aware)
+        self.validity_aware_min = validity_aware_min
         self.vocab_rows = vocab_rows
         self.device = torch.device(device)
         self.max_ws = max_ws
@@ -118,6 +120,8 @@ class FSMRegistry:
 
     def compile(self, schema: Dict) -> str:
         """CPU compile (any thread); returns the schema key for `install`."""
+        if self.validity_aware_min > 0:
+            schema = validity_aware(schema, self.validity_aware_min)
         key = self.key_of(schema)
         if key in self._fsms:  # lock-free hit: entries are published fully built
             return key

@@ -24,8 +24,9 @@ HEX = Cls(byte_mask((0x30, 0x39), (0x41, 0x46), (0x61, 0x66)))
 CONT = Cls(byte_mask((0x80, 0xBF)))
 
 
-def _string_char() -> Node:
-    ascii_ok = Cls(byte_mask((0x20, 0x7F)) & ~chars_mask(b'"\\'))
+def _string_char_parts() -> List[Node]:
+    """The alternatives of one JSON string character other than plain ASCII: an escape, and
+    2- / 3- / 4-byte UTF-8 sequences."""
     escape = seq(lit("\\"), alt(Cls(chars_mask(b'"\\/bfnrt')), seq(lit("u"), HEX, HEX, HEX, HEX)))
     two = seq(Cls(byte_mask((0xC2, 0xDF))), CONT)
     three = alt(seq(lit(b"\xe0"), Cls(byte_mask((0xA0, 0xBF))), CONT),
@@ -35,10 +36,40 @@ def _string_char() -> Node:
     four = alt(seq(lit(b"\xf0"), Cls(byte_mask((0x90, 0xBF))), CONT, CONT),
                seq(Cls(byte_mask((0xF1, 0xF3))), CONT, CONT, CONT),
                seq(lit(b"\xf4"), Cls(byte_mask((0x80, 0x8F))), CONT, CONT))
-    return alt(ascii_ok, escape, two, three, four)
+    return [escape, two, three, four]
 
 
-STRING_CHAR = _string_char()
+_STRING_CHAR_NON_ASCII = _string_char_parts()
+STRING_CHAR = alt(Cls(byte_mask((0x20, 0x7F)) & ~chars_mask(b'"\\')), *_STRING_CHAR_NON_ASCII)
+# a character Python's str.strip() never removes: printable ASCII other than space (and the
+# two that need escaping); escapes and non-ASCII characters do not count as visible
+VISIBLE_CHAR = Cls(byte_mask((0x21, 0x7E)) & ~chars_mask(b'"\\'))
+
+# JSON-schema extension keyword of the benchmark's validity-aware grammar: a string carries at
+# least this many visible characters (VISIBLE_CHAR), anywhere in it
+MIN_VISIBLE = "x-min-visible"
+
+
+def validity_aware(schema: Dict, min_visible: int = 10) -> Dict:
+    """The benchmark grammar for untrained weights (engine option ``validity_aware_json``):
+    every object property is emitted (optional ones made required) and every free-text string
+    (no enum / const) carries >= `min_visible` visible characters -- the simulator's own validity
+    rules for a decision (strategy >= 3, reasoning >= 10 stripped characters, reference
+    main.py:232-247) then hold for every output, as they do for a trained model's; a random
+    model under the plain grammar closes strings early or skips optional fields, and those
+    outputs go down the retry ladder.  Idempotent (TP followers re-apply it to the key)."""
+    if not isinstance(schema, dict):
+        return schema
+    out = dict(schema)
+    for key in ("anyOf", "oneOf"):
+        if key in out:
+            out[key] = [validity_aware(s, min_visible) for s in out[key]]
+    if out.get("type") == "object" and "properties" in out:
+        out["properties"] = {k: validity_aware(v, min_visible) for k, v in out["properties"].items()}
+        out["required"] = list(out["properties"])
+    if out.get("type") == "string" and "enum" not in out and "const" not in out:
+        out[MIN_VISIBLE] = max(int(out.get(MIN_VISIBLE, 0)), min_visible)
+    return out
 
 
 def _same_len_range(a: str, b: str) -> Node:
@@ -111,6 +142,12 @@ class SchemaCompiler:
             return alt(*[self.node({**schema, "type": k}) for k in kind])
         if kind == "object":
             return self.object_node(schema)
+        if kind == "string" and schema.get(MIN_VISIBLE):
+            # (invisible chars* visible){k} then any chars: >= k visible characters
+            k = int(schema[MIN_VISIBLE])
+            invisible = alt(Cls(chars_mask(b" \x7f")), *_STRING_CHAR_NON_ASCII)
+            body = seq(Rep(seq(Star(invisible), VISIBLE_CHAR), k, k), Star(STRING_CHAR))
+            return seq(lit('"'), body, lit('"'))
         if kind == "string":
             n = schema.get("maxLength")
             body = Rep(STRING_CHAR, int(schema.get("minLength", 0)), int(n)) if n is not None else (

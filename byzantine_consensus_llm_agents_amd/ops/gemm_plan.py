@@ -29,6 +29,7 @@ W4_CFG = 11  # csrc/kernels/gemm_w4.hip: 256 x 256, four 128 x 128 waves (one pe
 BIG_CFGS = (PP_CFG, W4_CFG)  # 256 x 256 tiles (the register-staged form lost its A/B: csrc/experimental/gemm_rs.hip)
 N_CFGS = len(TILES)
 SPLITS = (1, 2, 3, 4, 6, 8)
+STREAM_K = 0  # split_k value of the W4 kernel's stream-K launch (one workgroup per CU over tiles x K-tiles)
 
 
 class GemmPlan:
@@ -55,6 +56,11 @@ class GemmPlan:
                 self.timings[tuple(map(int, key.split(",")))] = times
 
     def supported(self, cfg: int, M: int, N: int, K: int, epi: int, split_k: int = 1) -> bool:
+        if split_k == STREAM_K:  # W4 only: 4 arrival counters per tile, 32-bit unit arithmetic
+            tiles = -(-M // 256) * -(-N // 256)
+            if cfg != W4_CFG or 4 * tiles > 1 << 16 or tiles * (K // 64) * 256 >= 1 << 31:
+                return False
+            split_k = 1
         if cfg not in self.tiles or M <= 0 or K % 64 or K <= 0 or split_k < 1 or K // 64 < split_k:
             return False
         bn = self.tiles[cfg][1]

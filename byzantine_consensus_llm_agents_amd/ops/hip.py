@@ -257,12 +257,23 @@ def hip_ops() -> SimpleNamespace:
              "split-K counters must be allocated outside graph capture (ops.prepare_device)")
         return torch.zeros(1 << 16, dtype=torch.int32, device=dev)
 
+    sk_ws = {}  # device index -> fp32 [2 x CUs x 65536]: stream-K parts (W4, split_k == 0)
+
     def prepare_device(dev):
         dev = torch.device(dev)
         if dev.index is None:
             dev = torch.device("cuda", torch.cuda.current_device())
         if dev.index not in counters:
             counters[dev.index] = _new_counters(dev)
+        if dev.index not in sk_ws:  # (128 MiB; allocated outside any graph capture)
+            with torch.cuda.device(dev):
+                sk_ws[dev.index] = torch.empty(lib.bcg_gemm_w4_sk_ws_floats(), dtype=torch.float32, device=dev)
+
+    def _sk_workspace(dev):
+        dev = torch.device("cuda", dev.index if dev.index is not None else torch.cuda.current_device())
+        if dev.index not in sk_ws:
+            prepare_device(dev)  # raises under capture (the counters' check)
+        return sk_ws[dev.index]
 
     def register_stream(stream):
         """Give `stream` its own split-K counters (its GEMMs may overlap the main stream's)."""
@@ -301,7 +312,9 @@ def hip_ops() -> SimpleNamespace:
             _req(residual is not None and residual.shape == (M, N) and residual.is_contiguous()
                  and residual.dtype == torch.bfloat16, "gemm_nt: residual [M,N] bf16")
         ws = cnt = None
-        if split_k > 1:
+        if split_k == 0:  # W4 stream-K: the device's persistent part buffer + the counters
+            ws, cnt = _sk_workspace(x.device), _counters(x.device)
+        elif split_k > 1:
             bm, bn = plan.tiles[cfg]
             tiles = (M + bm - 1) // bm * ((N + bn - 1) // bn)
             _req(tiles <= (1 << 16), "gemm_nt: too many output tiles for split-K")

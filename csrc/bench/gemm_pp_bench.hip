@@ -101,6 +101,10 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&ws, (size_t)tiles * split * 65536 * 4));
     CK(hipMalloc(&cnt, (size_t)tiles * 4));
     CK(hipMemset(cnt, 0, (size_t)tiles * 4));
+  } else if (split == 0) {  // W4 stream-K: 2 parts per CU, 4 counters per tile
+    CK(hipMalloc(&ws, (size_t)2 * 256 * 65536 * 4));
+    CK(hipMalloc(&cnt, (size_t)tiles * 16));
+    CK(hipMemset(cnt, 0, (size_t)tiles * 16));
   }
   auto run = [&](int i) {
     const void* res = epi == 2 ? r : nullptr;

@@ -210,36 +210,69 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       return static_cast<uint32_t>(t & 1) * STAGE + part * A_BYTES;
   };
 
-  // ---- work items: nwg = tiles x k-splits.  A persistent launch (gridDim.x < nwg, split_k == 1
-  // only) gives workgroup b the items b, b + G, b + 2G, ...: one continuous stream of K-tiles in
-  // which the next item's first tiles are already in flight while this item's epilogue runs.
-  // Item -> tile: XCD-aware bijective remap (item i runs on XCD i % 8 when G % 8 == 0, so each
-  // XCD's CUs walk one contiguous range of remapped ids), grouped m-tiles, then (tile, k-split).
-  const int nwg = m_tiles * n_tiles * split_k;
+  // ---- work items.  split_k >= 1: nwg = tiles x k-splits.  A persistent launch (gridDim.x <
+  // nwg, split_k == 1 only) gives workgroup b the items b, b + G, b + 2G, ...: one continuous
+  // stream of K-tiles in which the next item's first tiles are already in flight while this
+  // item's epilogue runs.  Item -> tile: XCD-aware bijective remap (item i runs on XCD i % 8 when
+  // G % 8 == 0, so each XCD's CUs walk one contiguous range of remapped ids), grouped m-tiles,
+  // then (tile, k-split).
+  // split_k == 0: stream-K.  The tiles x K-tiles units are cut into G equal contiguous ranges;
+  // logical workgroup r (XCD-grouped: the workgroups of one XCD own one contiguous eighth of
+  // the units) streams range r -- a partial first tile, whole tiles, a partial last tile.
+  // Whole tiles take the ordinary in-stream epilogue; a partial segment stores its fp32 part
+  // (per wave, write-through) and the wave that arrives last for that (tile, wave) adds every
+  // segment's part after its stream and runs the epilogue -- nobody waits on another workgroup.
+  // The tile quantisation of decode-size M goes away (gate_up at 704 rows: 408 tiles = 1.6 per
+  // CU instead of two rounds).
+  const bool sk = split_k == 0;
+  const int nsplit = sk ? 1 : split_k;
+  const int tiles = m_tiles * n_tiles;
+  const int nwg = tiles * nsplit;
   const int G = gridDim.x;
-  const int n_items = (nwg - 1 - static_cast<int>(blockIdx.x)) / G + 1;
+  const int nk_all = K / (128 / ESZ);  // K-tiles of 128 B per row
+  int r_wg = blockIdx.x;               // stream-K: the logical workgroup (bijective XCD grouping)
+  if (sk) {
+    const int b = blockIdx.x, xcd = b & 7, q = G >> 3, rem = G & 7;
+    r_wg = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+  }
+  // (32-bit: the host keeps tiles x nk_all x G below 2^31)
+  auto sk_u0 = [&](int r) { return static_cast<int>(static_cast<uint32_t>(r) * (tiles * nk_all) / G); };
+  const int u0 = sk ? sk_u0(r_wg) : 0, u1 = sk ? sk_u0(r_wg + 1) : 0;
+  const int T0 = u0 / nk_all;
+  const int n_items = sk ? (u1 > u0 ? (u1 - 1) / nk_all - T0 + 1 : 0)
+                         : (nwg - 1 - static_cast<int>(blockIdx.x)) / G + 1;
   struct Geo {
-    int m0, n0, tile, split;
+    int m0, n0, tile, split, k0, nk;  // output corner, tile id, k-split, first K-tile and K-tiles of the item
   };
-  auto geo = [&](int j) {
-    const int i = blockIdx.x + j * G;
-    const int xcd = i & 7, q = nwg >> 3, rem = nwg & 7;
-    const int r_id = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (i >> 3);
-    Geo g;
-    g.split = r_id % split_k;
-    g.tile = r_id / split_k;
+  auto tile_geo = [&](Geo& g) {
     constexpr int GM = F8 ? W4_GROUP_M_F8 : W4_GROUP_M;
     const int grp = g.tile / (GM * n_tiles), in_grp = g.tile % (GM * n_tiles);
     const int gm = min(m_tiles - grp * GM, GM);
     g.m0 = (grp * GM + in_grp % gm) * BM;
     g.n0 = (in_grp / gm) * BN;
+  };
+  auto geo = [&](int j) {
+    Geo g;
+    if (sk) {
+      g.tile = T0 + j;
+      g.split = 0;
+      const int s0 = max(u0, g.tile * nk_all), e0 = min(u1, (g.tile + 1) * nk_all);
+      g.k0 = s0 - g.tile * nk_all;
+      g.nk = e0 - s0;
+    } else {
+      const int i = blockIdx.x + j * G;
+      const int xcd = i & 7, q = nwg >> 3, rem = nwg & 7;
+      const int r_id = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (i >> 3);
+      g.split = r_id % split_k;
+      g.tile = r_id / split_k;
+      g.k0 = g.split * nk_all / split_k;
+      g.nk = (g.split + 1) * nk_all / split_k - g.k0;
+    }
+    tile_geo(g);
     return g;
   };
-  Geo gc = geo(0);                     // the item whose accumulators are live
-  const int nk_all = K / (128 / ESZ);  // K-tiles of 128 B per row
-  const int kt0 = gc.split * nk_all / split_k;
-  const int nk = (gc.split + 1) * nk_all / split_k - kt0;  // (all items alike: split_k == 1 when persistent)
-  const int total = n_items * nk;                           // K-tiles of the stream
+  Geo gc = geo(0);                                     // the item whose accumulators are live
+  const int total = sk ? u1 - u0 : n_items * gc.nk;    // K-tiles of the stream
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -276,10 +309,12 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   auto dma_m0 = [&](int t, int q) {
     return __builtin_amdgcn_readfirstlane(lds_base + slot_off(t, q >= 8) + (q & 7) * 4096 + wave * 1024);
   };
-  // stream tile t = K-tile kt of its item; mode 0: M0 write + piece in one statement; 1: the
-  // piece only (M0 set earlier: set_m0)
+  // DMA cursor: stream tile t + 2 is K-tile dk0 + ktd of item jd, whose descriptors are dX / dW
+  int jd = 0, ktd = 0, dk0 = gc.k0, dnk = gc.nk;
+  // stream tile t = K-tile kt of the DMA cursor's item; mode 0: M0 write + piece in one
+  // statement; 1: the piece only (M0 set earlier: set_m0)
   auto dma = [&](int t, int kt, int q, const i32x4& sX, const i32x4& sW, int mode = 0) {
-    const uint32_t kb = static_cast<uint32_t>(kt0 + kt) * (BK * 2);
+    const uint32_t kb = static_cast<uint32_t>(dk0 + kt) * (BK * 2);
     const bool isx = q < 8;
     const int i = q & 7;
     const uint32_t soff = __builtin_amdgcn_readfirstlane(kb);
@@ -370,22 +405,24 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   };
 
   bf16x8 x0[8], w0[8], x1[8], w1[8];
-  // DMA cursor: stream tile t + 2 is K-tile ktd of item jd, whose descriptors are dX / dW
   i32x4 dX, dW;
   item_srd(gc, dX, dW);
   i32x4 nullX = dX, nullW = dW;  // zero-range descriptors: pieces past the stream's last tile
   nullX[2] = 0, nullW[2] = 0;
-  int jd = 0, ktd = 0;
   auto advance = [&]() {
-    if (++ktd == nk) {
+    if (++ktd == dnk) {
       ktd = 0;
-      if (++jd < n_items) item_srd(geo(jd), dX, dW);
+      if (++jd < n_items) {
+        const Geo g = geo(jd);
+        item_srd(g, dX, dW);
+        dk0 = g.k0, dnk = g.nk;
+      }
     }
   };
 #ifdef W4_DESYNC  // timing experiment: odd workgroups start nk x W4_DESYNC cycles late (epilogues staggered)
   if (blockIdx.x & 1) {
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
-    while (__builtin_amdgcn_s_memtime() - t0 < static_cast<uint64_t>(nk) * W4_DESYNC) __builtin_amdgcn_s_sleep(10);
+    while (__builtin_amdgcn_s_memtime() - t0 < static_cast<uint64_t>(gc.nk) * W4_DESYNC) __builtin_amdgcn_s_sleep(10);
   }
 #endif
   // ---- prologue: stream tiles 0 and 1 in flight, tile 0 landed, k-step 0 of tile 0 in registers ----
@@ -785,6 +822,103 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       }
   };
 
+  // ---- fp32 parts of a tile (split-K slabs, stream-K segments): per (wave, block, 16-B quarter)
+  // 256 floats, lane-major, so a wave's 64 pieces are one contiguous 64 KiB and a piece lands
+  // lane-linearly exactly where that lane reads it back.
+  constexpr int QPB = L32 ? 4 : 1;  // 16-B quarters per block per lane
+  static_assert(NB * NB * QPB == 64, "64 pieces of 1 KiB per wave and part");
+  auto piece_off = [&](int i, int j, int qq) {  // this lane's 16 B of block (i, j), quarter qq
+    return static_cast<uint32_t>((((wave * NB + i) * NB + j) * QPB + qq) * 1024 + lane * 16);
+  };
+  // acc += the n parts at byte offsets off_of(k) (k < n) of `srd`: LDS-DMA rounds of 16 pieces
+  // per wave into two alternating 16-KiB buffers of this wave (a round in flight while the
+  // previous one is added) -- many loads in flight, no VGPRs held for them.  The caller has
+  // retired every other use of the wave's LDS region; the parts were stored write-through (sc1)
+  // and every load of them is sc1.
+  auto add_parts = [&](float* base_ptr, uint32_t bytes, int n, auto off_of) {
+    const i32x4 srd = make_srd(base_ptr, bytes);
+    const uint32_t lds_w = lds_base + static_cast<uint32_t>(wave) * 16384;
+    auto issue = [&](int k, int g, int b) {
+      const uint32_t base = off_of(k) + static_cast<uint32_t>(wave * 64 + 16 * g) * 1024;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const uint32_t soff = __builtin_amdgcn_readfirstlane(base + q * 1024);
+        const uint32_t m0v = __builtin_amdgcn_readfirstlane(lds_w + b * 65536 + q * 1024);
+        asm volatile("s_mov_b32 m0, %3\n\tbuffer_load_dwordx4 %0, %1, %2 offen sc1 lds"
+                     :
+                     : "v"(static_cast<uint32_t>(lane) * 16), "s"(srd), "s"(soff), "s"(m0v)
+                     : "memory", "m0");
+      }
+    };
+    auto consume = [&](int g, int b) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int f = 16 * g + q, i = f / (NB * QPB), j = (f / QPB) % NB, qq = f % QPB;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(smem + wave * 16384 + b * 65536 + q * 1024 + lane * 16);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float a;
+          asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(a) : "a"(acc[i][j][4 * qq + e]));
+          a += v[e];
+          asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(acc[i][j][4 * qq + e]) : "v"(a));
+        }
+      }
+      // these reads are done before the round after next refills buffer b
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+    if (n > 0) issue(0, 0, 0);
+    for (int k = 0; k < n; ++k) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {  // (4 rounds per part: the buffer index g & 1 is static)
+        if (g < 3)
+          issue(k, g + 1, (g + 1) & 1);
+        else if (k + 1 < n)
+          issue(k + 1, 0, 0);
+        if (g < 3 || k + 1 < n)
+          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // this round landed, the next in flight
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        consume(g, g & 1);
+      }
+    }
+    asm volatile("s_nop 4" ::: "memory");  // (AGPR writes -> the epilogue's reads)
+  };
+  // stream-K: the logical workgroup whose range holds unit u; the tile's segments are those of
+  // workgroups wg_of(T nk) .. wg_of((T + 1) nk - 1), segment (r, T) stored in part 2 r + (T is
+  // r's first tile ? 0 : 1)
+  auto wg_of = [&](int u) {
+    return static_cast<int>((static_cast<uint32_t>(u + 1) * G - 1) / static_cast<uint32_t>(tiles * nk_all));
+  };
+  auto nseg = [&](int T) { return wg_of((T + 1) * nk_all - 1) - wg_of(T * nk_all) + 1; };
+  auto sk_part = [&](int r, int T) { return static_cast<uint32_t>(2 * r + (T == sk_u0(r) / nk_all ? 0 : 1)) * (BM * BN * 4); };
+  // a partial stream-K segment (in the stream): store this wave's fp32 part.  Counting the
+  // segments (and reducing) waits for the end of the stream: bookkeeping inside the K-loop's
+  // item-end block made hipcc spill the accumulators.
+  auto sk_partial = [&](const Geo& g) {
+    if constexpr (!L32) {
+      // (the lane index re-enters through an opaque move, as in the epilogue: per-lane offsets
+      // hoisted out of the K-loop would hold VGPRs across it and spill)
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const uint32_t lane_off = static_cast<uint32_t>(wave * 64 * 1024 + ln * 16);
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(ws, 0, static_cast<uint32_t>(2 * G) * (BM * BN * 4), 0x00020000);
+      const uint32_t part = sk_part(r_wg, g.tile);
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const auto v = read_acc(acc[i][j]);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs,
+                                                 lane_off + static_cast<uint32_t>(i * NB + j) * 1024, part,
+                                                 16 /*sc1*/);
+          // one block at a time: hoisting every accumulator read above the stores would need
+          // the whole tile in VGPRs inside the K-loop (spills)
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  };
+
   // phase B of stream tile t (W pieces of tile t + 2 = K-tile kt2 of its item).  Past the last
   // tile the pieces go through a zero-range descriptor: no memory traffic, the zeros land in a
   // stage nobody reads -- branch-free, one body (a branch around the pieces, or two copies of
@@ -858,8 +992,8 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         // of all 256 CUs saturate.  The sink VGPR stays live through the loop; its previous
         // load is older than the 8 pieces the barrier's vmcnt(8) leaves, so it has landed.
         asm volatile("" : : "v"(pf_sink));
-        const int r = ktc - (nk - W4_RES_PF);
-        if (split_k == 1 && r >= 0 && r % (W4_RES_PF / 4) == 0) {
+        const int r = ktc - (gc.nk - W4_RES_PF);
+        if (nsplit == 1 && r >= 0 && r % (W4_RES_PF / 4) == 0) {
           const int line = (r / (W4_RES_PF / 4)) * 256 + tid;
           const int row = min(gc.m0 + (line >> 2), M - 1), col = min(gc.n0 + (line & 3) * 64, N - 2);
           const bf16_t* pf = residual + static_cast<size_t>(row) * ldc + col;
@@ -872,11 +1006,14 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       t_end = __builtin_amdgcn_s_memtime();
       cyc_b += t_end - t_w;
 #endif
-      if (split_k == 1 && ++ktc == nk) {
+      if (nsplit == 1 && ++ktc == gc.nk) {
         // item done: its epilogue runs while the next item's first two K-tiles land.  The last
         // MFMAs' results are read by VALU / stores: cover the MFMA D -> read hazard first.
         asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
-        epilogue(gc, [&](int i, int j) { return read_acc(acc[i][j]); }, W4_STAGE_EPI && W4_RING5 ? slot_off(t, 1) : 0xffffffffu);
+        if (gc.nk == nk_all)
+          epilogue(gc, [&](int i, int j) { return read_acc(acc[i][j]); }, W4_STAGE_EPI && W4_RING5 ? slot_off(t, 1) : 0xffffffffu);
+        else
+          sk_partial(gc);  // (stream-K: a tile cut by this workgroup's range)
 #if W4_STAGE_EPI && W4_RING5
         // every wave's staging reads are done before phase A(t+1) loads X(t+3) into that slot
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -920,6 +1057,47 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   }
   // every piece (the zero-range ones past the end included) has landed before the wave ends
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if (sk) {
+    if constexpr (!L32) {
+      __syncthreads();  // every wave's stream is over: the LDS ring is free for the part rounds
+      // this workgroup's first and last item, when partial (straight-line code: a loop around
+      // the reduction made hipcc spill)
+      auto reduce_item = [&](int j) {
+        const Geo gp = geo(j);
+        if (gp.nk == nk_all) return;  // a whole tile: its epilogue ran in the stream
+        const int T = gp.tile;
+        // this wave's part of T is stored (sc1, drained); the wave that counts last for (T,
+        // wave) over the tile's segments sums them
+        int last = 0;
+        if (lane == 0) {
+          int* cnt = counters + T * 4 + wave;
+          last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nseg(T) - 1;
+          if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (!__builtin_amdgcn_readlane(last, 0)) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        // zeros by VALU writes, not zero_acc's MFMAs: out here hipcc spills and reloads
+        // accumulators between the asm statements, and its spill store of an asm MFMA's result
+        // gets no wait states (it read some 16-lane rows before the MFMA had written them)
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+#pragma unroll
+          for (int jj = 0; jj < NB; ++jj)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) asm volatile("v_accvgpr_write_b32 %0, 0" : "=a"(acc[i][jj][e]));
+        const int rf = wg_of(T * nk_all), rl = wg_of((T + 1) * nk_all - 1);
+        add_parts(ws, static_cast<uint32_t>(2 * G) * (BM * BN * 4), rl - rf + 1,
+                  [&](int k) { return sk_part(rf + k, T); });
+        Geo g;
+        g.tile = T;
+        tile_geo(g);
+        epilogue(g, [&](int i, int jj) { return read_acc(acc[i][jj]); });
+      };
+      if (n_items > 0) reduce_item(0);
+      if (n_items > 1) reduce_item(n_items - 1);
+    }
+    return;
+  }
   if (split_k == 1) return;  // (the epilogues ran in the stream)
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
 
@@ -932,8 +1110,6 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   // rows, profiles/r5_gemm_feed.)  Slab layout: per (wave, block, 16-B quarter) 256 floats,
   // lane-major, so a wave's 64 pieces are one contiguous 64 KiB and a piece lands lane-linearly
   // exactly where that lane reads it back.
-  constexpr int QPB = L32 ? 4 : 1;  // 16-B quarters per block per lane
-  static_assert(NB * NB * QPB == 64, "64 pieces of 1 KiB per wave and slab");
   float* slab = ws + static_cast<size_t>(gc.tile) * split_k * (BM * BN);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, split_k * BM * BN * 4, 0x00020000);
   __syncthreads();  // every wave is past its last ds_read: smem is reusable as the flag slot
@@ -981,56 +1157,9 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (and every slab load is sc1)
-  const i32x4 srd = make_srd(slab, static_cast<uint32_t>(split_k) * BM * BN * 4);
-  const uint32_t lds_w = lds_base + static_cast<uint32_t>(wave) * 16384;
-  // round = 16 pieces (f = 16 g ..) of split sp into buffer b (2 x 64 KiB: 4 waves x 16 KiB)
-  auto issue = [&](int sp, int g, int b) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const uint32_t soff = __builtin_amdgcn_readfirstlane(
-          static_cast<uint32_t>(sp) * (BM * BN * 4) + static_cast<uint32_t>(wave * 64 + 16 * g + q) * 1024);
-      const uint32_t m0v = __builtin_amdgcn_readfirstlane(lds_w + b * 65536 + q * 1024);
-      asm volatile("s_mov_b32 m0, %3\n\tbuffer_load_dwordx4 %0, %1, %2 offen sc1 lds"
-                   :
-                   : "v"(static_cast<uint32_t>(lane) * 16), "s"(srd), "s"(soff), "s"(m0v)
-                   : "memory", "m0");
-    }
-  };
-  auto consume = [&](int g, int b) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int f = 16 * g + q, i = f / (NB * QPB), j = (f / QPB) % NB, qq = f % QPB;
-      const f32x4 v = *reinterpret_cast<const f32x4*>(smem + wave * 16384 + b * 65536 + q * 1024 + lane * 16);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float a;
-        asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(a) : "a"(acc[i][j][4 * qq + e]));
-        a += v[e];
-        asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(acc[i][j][4 * qq + e]) : "v"(a));
-      }
-    }
-    // these reads are done before the round after next refills buffer b
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  };
-  const int first = gc.split == 0 ? 1 : 0;  // the other splits, in order
-  if (first < split_k) issue(first, 0, 0);
-  for (int sp = first; sp < split_k; sp = (sp + 1 == gc.split ? sp + 2 : sp + 1)) {
-    const int nsp = sp + 1 == gc.split ? sp + 2 : sp + 1;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {  // (4 rounds per split: the buffer index g & 1 is static)
-      if (g < 3)
-        issue(sp, g + 1, (g + 1) & 1);
-      else if (nsp < split_k)
-        issue(nsp, 0, 0);
-      const bool more = g < 3 || nsp < split_k;
-      if (more)
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // this round landed, the next in flight
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      consume(g, g & 1);
-    }
-  }
-  asm volatile("s_nop 4" ::: "memory");  // (AGPR writes -> the epilogue's reads)
+  add_parts(slab, static_cast<uint32_t>(split_k) * BM * BN * 4, split_k - 1, [&](int k) {  // the other splits
+    return static_cast<uint32_t>(k < gc.split ? k : k + 1) * (BM * BN * 4);
+  });
   epilogue(gc, [&](int i, int j) { return read_acc(acc[i][j]); });
 }
 
@@ -1044,15 +1173,20 @@ int w4_cus() {
   return cus[dev] > 0 ? cus[dev] : 256;
 }
 
+// stream-K grid: one workgroup per CU, never more than there are K-tile units
+int w4_sk_grid(int tiles, int nk_all) { return static_cast<int>(std::min<long long>(w4_cus(), 1ll * tiles * nk_all)); }
+
 template <int EPI, bool F8 = false>
 int launch_w4(const void* x, const void* w, const void* bias, const void* res, void* c, float* ws, int* cnt, int M,
               int N, int K, int inter, int split_k, hipStream_t stream, const float* xs = nullptr,
               const float* wsc = nullptr) {
   const int m_tiles = (M + BM - 1) / BM, n_tiles = (N + BN - 1) / BN;
   const int ldc = EPI == EPI_SILU_MUL ? inter : N;
-  const int nwg = m_tiles * n_tiles * split_k;
-  // persistent: one workgroup per CU streams its items (split_k == 1 only)
-  const int grid = W4_PERSIST && split_k == 1 ? std::min(nwg, w4_cus()) : nwg;
+  const int nwg = m_tiles * n_tiles * std::max(split_k, 1);
+  // persistent: one workgroup per CU streams its items (split_k == 1), or its range of the
+  // tiles x K-tiles units (split_k == 0, stream-K)
+  const int grid = split_k == 0 ? w4_sk_grid(m_tiles * n_tiles, K / (F8 ? 128 : BK))
+                   : W4_PERSIST && split_k == 1 ? std::min(nwg, w4_cus()) : nwg;
   hipLaunchKernelGGL((gemm_w4_kernel<EPI, !F8 && W4_MFMA32 != 0, F8>), dim3(grid), dim3(256),
                      0, stream, x, w, static_cast<const bf16_t*>(bias), static_cast<const bf16_t*>(res),
                      static_cast<bf16_t*>(c), ws, cnt, M, N, K, ldc, inter, m_tiles, n_tiles, split_k, xs, wsc);
@@ -1072,14 +1206,22 @@ BCG_API int bcg_gemm_w4_stamps(void* host, int n) {
 // 2 = residual + acc.  K % 64 == 0, K/64 >= split_k; N % 16 == 0 (a partial last n-tile is
 // masked); EPI 1: N == 2*inter, inter % 128 == 0.  split_k > 1: `ws` >= m_tiles*n_tiles*
 // split_k*65536 floats, `counters` >= m_tiles*n_tiles zeroed ints (left zeroed).
+// split_k == 0: stream-K (one workgroup per CU over the tiles x K-tiles units): `ws` >=
+// bcg_gemm_w4_sk_ws_floats() floats, `counters` >= 4*m_tiles*n_tiles zeroed ints (left zeroed).
+BCG_API int bcg_gemm_w4_sk_ws_floats() { return 2 * w4_cus() * BM * BN; }
+
 BCG_API int bcg_gemm_w4(int epi, const void* x, const void* w, const void* bias, const void* residual, void* c,
                         void* ws, void* counters, int M, int N, int K, int inter, int split_k, hipStream_t stream) {
-  if (M <= 0 || N <= 0 || N % 16 || K % BK || K <= 0 || split_k < 1 || K / BK < split_k) return -2;
+  if (M <= 0 || N <= 0 || N % 16 || K % BK || K <= 0 || split_k < 0 || K / BK < split_k) return -2;
   // 32-bit buffer offsets, rows up to a whole tile past the end included
   if (2ull * (M + BM) * K >= (1ull << 31) || 2ull * (N + BN) * K >= (1ull << 31)) return -2;
   // the output (and residual) offsets, a masked column's 0x80000000 bias included, stay 32-bit
   if (2ull * (M + BM) * (epi == EPI_SILU_MUL ? inter : N) >= (1ull << 31)) return -2;
-  if (split_k > 1 && (!ws || !counters)) return -2;
+  if (split_k != 1 && (!ws || !counters)) return -2;
+  if (split_k == 0) {  // stream-K: 4 counters per tile; the kernel's unit arithmetic is 32-bit
+    const long long tiles = 1ll * ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    if (4 * tiles > (1 << 16) || tiles * (K / BK) * w4_cus() >= (1ll << 31)) return -2;
+  }
   float* wsf = static_cast<float*>(ws);
   int* cnt = static_cast<int*>(counters);
   switch (epi) {

@@ -222,3 +222,25 @@ def test_prefill_carry_matches_reference(fresh_engine_state):
     got, stats = run(4)
     assert len(got) == 18 and got == ref
     assert stats["prefill_carried"] > 0 and stats["prefill_full_chunks"] > 0
+
+
+def test_validity_aware_grammar_outputs_pass_simulator_rules(fresh_engine_state):
+    """The bench grammar on the real engine (torch ops, random tiny Qwen3, budget-aware
+    sampling): every decide output passes the simulator's batched validity rule -- none would
+    go down the retry ladder -- and every vote is in its enum."""
+    import json
+    from byzantine_consensus_llm_agents_amd.bcg import prompts as P
+    from byzantine_consensus_llm_agents_amd.bcg.simulation import is_valid_decision, is_valid_vote
+    from byzantine_consensus_llm_agents_amd.engine import GuidedDecodingParams, LLM, SamplingParams
+    llm = LLM("bcg/tiny-qwen3", backend="torch", seed=11, max_model_len=1024, kv_cache_gb=0.05,
+              max_batch_seqs=16, budget_aware_json=True, validity_aware_json=10)
+    schemas = [P.honest_decision_schema(0, 50), P.byzantine_decision_schema(0, 50),
+               P.vote_schema(P.HONEST_VOTE_OPTIONS)]
+    params = [SamplingParams(temperature=1.0, max_tokens=[150, 150, 40][i % 3],
+                             guided_decoding=GuidedDecodingParams(json=schemas[i % 3])) for i in range(15)]
+    outs = llm.generate([f"<|im_start|>user\nagent_{i} round 2<|im_end|>\n<|im_start|>assistant\n"
+                         for i in range(15)], params)
+    llm.shutdown()
+    for i, o in enumerate(outs):
+        obj = json.loads(o.outputs[0].text)
+        assert is_valid_vote(obj) if i % 3 == 2 else is_valid_decision(obj), obj

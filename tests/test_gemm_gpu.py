@@ -298,3 +298,35 @@ def test_gemm_fp8_big_tile_partial_m_leaves_rows_past_m(hip, cfg, epi, M):
     got = hip.gemm_nt_fp8(xq, xs, wq, ws, cfg, epi, residual=res, out=buf[:M])
     _close(got, ref)
     assert torch.all(buf[M:] == 7.0), "rows past M were written"
+
+
+@pytest.mark.parametrize("M,N,K", [(37, 512, 1024), (704, 1040, 5120), (257, 34816 // 8, 640), (2048 + 77, 1536, 2048),
+                                   (704, 7168, 5120), (1, 256, 128)])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+def test_gemm_w4_stream_k(hip, M, N, K, epi):
+    """W4 stream-K (split_k = 0): one workgroup per CU over the tiles x K-tiles units, partial
+    tiles summed by the last-arriving wave after its stream.  Store + bias, SiLU, residual in
+    place (bias too); rows past M untouched; repeated launches (counters left zeroed)."""
+    torch.manual_seed(M + N + epi)
+    if epi == 1 and (N // 2) % 128:
+        pytest.skip("silu: inter % 128")
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda").to(torch.bfloat16)
+    assert hip.gemm_plan.supported(11, M, N, K, epi, 0)
+    ref = _ref(x, w)
+    width = N // 2 if epi == 1 else N
+    for rep in range(3):
+        buf = torch.full((M + 256, width), 7.0, device="cuda", dtype=torch.bfloat16)
+        if epi == 0:
+            got = hip.gemm_nt(x, w, (11, 0), 0, bias=b, out=buf[:M])
+            want = ref + b.float()
+        elif epi == 1:
+            got = hip.gemm_nt(x, w, (11, 0), 1, out=buf[:M])
+            want = torch.nn.functional.silu(ref[:, :width]) * ref[:, width:]
+        else:
+            buf[:M] = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+            want = ref + buf[:M].float() + b.float()
+            got = hip.gemm_nt(x, w, (11, 0), 2, bias=b, residual=buf[:M], out=buf[:M])
+        _close(got, want)
+        assert torch.all(buf[M:] == 7.0), "rows past M were written"

@@ -124,3 +124,38 @@ def test_block_manager_partial_prompt_never_fully_cached():
     bm.commit_prompt(list(a.blocks), prompt)
     b = bm.allocate(prompt, 1, True)
     assert b.ok and b.num_cached_tokens < len(prompt)
+
+
+def test_validity_aware_grammar_matches_simulator_rules():
+    """Benchmark grammar (engine validity_aware_json): every property emitted, free-text
+    strings with >= 10 visible characters; what it accepts passes the simulator's batched
+    validity rule, what it rejects includes the short / whitespace-only strings a random
+    model closes early; the transform is idempotent (TP followers re-apply it to the key)."""
+    import json
+    from byzantine_consensus_llm_agents_amd.bcg import prompts as P
+    from byzantine_consensus_llm_agents_amd.bcg.simulation import is_valid_decision
+    from byzantine_consensus_llm_agents_amd.engine.guided.json_schema import schema_to_dfa, validity_aware
+
+    def accepts(dfa, s):
+        st = 0
+        for b in s.encode():
+            st = int(dfa.trans[st, b])
+            if st < 0:
+                return False
+        return bool(dfa.accept[st])
+
+    hon, byz = P.honest_decision_schema(0, 50), P.byzantine_decision_schema(0, 50)
+    assert validity_aware(validity_aware(hon)) == validity_aware(hon)
+    assert validity_aware(P.vote_schema(P.HONEST_VOTE_OPTIONS)) == P.vote_schema(P.HONEST_VOTE_OPTIONS)
+    d, db = schema_to_dfa(validity_aware(hon)), schema_to_dfa(validity_aware(byz))
+    good = ['{"internal_strategy": "abcdefghij", "value": 7, "public_reasoning": "0123456789"}',
+            '{"internal_strategy": "a b c d e f g h i j", "value": 50, "public_reasoning": " 0123456789 \\n"}']
+    bad = ['{"internal_strategy": "abc", "value": 7, "public_reasoning": "0123456789"}',
+           '{"internal_strategy": "          \\n\\n", "value": 7, "public_reasoning": "0123456789"}',
+           '{"internal_strategy": "abcdefghij", "value": 7, "public_reasoning": "\\u00e9\\u00e9\\u00e9"}']
+    for s in good:
+        assert accepts(d, s) and is_valid_decision(json.loads(s))
+    for s in bad:
+        assert not accepts(d, s)
+    assert not accepts(db, '{"internal_strategy": "abcdefghij", "value": "abstain"}')  # reasoning now emitted
+    assert accepts(db, '{"internal_strategy": "abcdefghij", "value": "abstain", "public_reasoning": "0123456789"}')

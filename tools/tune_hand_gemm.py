@@ -27,7 +27,7 @@ import torch.nn.functional as F  # noqa: E402
 
 from byzantine_consensus_llm_agents_amd.models.config import ALIASES, get_model_config  # noqa: E402
 from byzantine_consensus_llm_agents_amd.ops import get_ops  # noqa: E402
-from byzantine_consensus_llm_agents_amd.ops.gemm_plan import BIG_CFGS, N_CFGS, SPLITS, TABLE  # noqa: E402
+from byzantine_consensus_llm_agents_amd.ops.gemm_plan import BIG_CFGS, N_CFGS, SPLITS, STREAM_K, TABLE, W4_CFG  # noqa: E402
 
 
 def shapes(cfg, tp):
@@ -122,7 +122,7 @@ def main():
                     continue
                 bm, bn = hip.gemm_plan.tiles[c]
                 tiles = -(-M // bm) * -(-N // bn)
-                for sk in SPLITS:
+                for sk in SPLITS + ((STREAM_K,) if c == W4_CFG else ()):  # (0 = W4 stream-K)
                     if M > 1024 and sk > 1:
                         continue
                     if only_cfgs and c not in only_cfgs and [c, sk] != list(prev):
