@@ -56,13 +56,15 @@ class GemmPlan:
                 self.timings[tuple(map(int, key.split(",")))] = times
 
     def supported(self, cfg: int, M: int, N: int, K: int, epi: int, split_k: int = 1) -> bool:
-        if split_k == STREAM_K:  # W4 only: 4 arrival counters per tile, 32-bit unit arithmetic
+        if split_k == STREAM_K:  # W4 only: an arrival counter per tile, 32-bit unit arithmetic
             tiles = -(-M // 256) * -(-N // 256)
-            if cfg != W4_CFG or 4 * tiles > 1 << 16 or tiles * (K // 64) * 256 >= 1 << 31:
+            if cfg != W4_CFG or tiles > 65024 or tiles * (K // 64) * 256 >= 1 << 31:
                 return False
             split_k = 1
         if cfg not in self.tiles or M <= 0 or K % 64 or K <= 0 or split_k < 1 or K // 64 < split_k:
             return False
+        if cfg == W4_CFG and split_k > 1 and -(-M // 256) * -(-N // 256) > 65024:
+            return False  # split-K arrival counters below the reduce-scatter scheme's slots
         bn = self.tiles[cfg][1]
         if cfg in BIG_CFGS:  # 32-bit buffer offsets: operands below 4 GiB (W4: 2 GiB), output below 2 GiB
             lim = 1 << (31 if cfg == W4_CFG else 32)

@@ -97,15 +97,16 @@ int main(int argc, char** argv) {
   const int tiles = (M + 255) / 256 * ((N + 255) / 256);
   float* ws = nullptr;
   int* cnt = nullptr;
-  if (split > 1) {
-    CK(hipMalloc(&ws, (size_t)tiles * split * 65536 * 4));
-    CK(hipMalloc(&cnt, (size_t)tiles * 4));
-    CK(hipMemset(cnt, 0, (size_t)tiles * 4));
-  } else if (split == 0) {  // W4 stream-K: 2 parts per CU, 4 counters per tile
-    CK(hipMalloc(&ws, (size_t)2 * 256 * 65536 * 4));
-    CK(hipMalloc(&cnt, (size_t)tiles * 16));
-    CK(hipMemset(cnt, 0, (size_t)tiles * 16));
+  // the framework's counter array: 65536 zeroed ints (the W4 reduce-scatter split-K keeps its
+  // arrival counters at the top of it)
+  if (split != 1) {
+    CK(hipMalloc(&cnt, (size_t)65536 * 4));
+    CK(hipMemset(cnt, 0, (size_t)65536 * 4));
   }
+  if (split > 1)
+    CK(hipMalloc(&ws, (size_t)tiles * split * 65536 * 4));
+  else if (split == 0)  // W4 stream-K: 2 parts per CU
+    CK(hipMalloc(&ws, (size_t)2 * 256 * 65536 * 4));
   auto run = [&](int i) {
     const void* res = epi == 2 ? r : nullptr;
     void* out = epi == 2 ? (void*)r : (void*)c;
