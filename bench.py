@@ -318,15 +318,22 @@ def thread_cpu():
         return {}
     names = {t.native_id: t.name for t in threading.enumerate()}
 
-    def group(name):
-        if name is None:
+    def native(tid):  # the OS thread name, its numeric suffix dropped: one group per pool
+        try:
+            with open(f"/proc/self/task/{tid}/comm") as f:
+                return "native:" + (f.read().strip().rstrip("0123456789-_ ") or "?")
+        except OSError:
             return "native"
+
+    def group(name, tid):
+        if name is None:
+            return native(tid)
         if name.startswith("sim"):
             return "game_threads"
         if name.startswith("bcg-engine") or name.startswith("bcg-tp"):
             return "engine"
         return "main" if name == "MainThread" else "python_other"
-    return {t.id: (group(names.get(t.id)), t.user_time + t.system_time) for t in psutil.Process().threads()}
+    return {t.id: (group(names.get(t.id), t.id), t.user_time + t.system_time) for t in psutil.Process().threads()}
 
 
 def thread_cpu_delta(before: dict, after: dict, total_s: float) -> dict:
@@ -509,6 +516,10 @@ def main(argv=None):
     t_start = time.perf_counter()
     cpu0 = time.process_time()  # this rank's host CPU (all threads) over the timed region
     thr0 = thread_cpu()
+    sampler = None
+    if os.environ.get("BCG_HOST_SAMPLE") == "1":  # where the host CPU goes (utils/host_sampler.py)
+        from byzantine_consensus_llm_agents_amd.utils.host_sampler import HostSampler
+        sampler = HostSampler().start()
     ctr0 = pool.counter_totals() if pool is not None else {}
     a0 = accepted()
     per_window, steps_done, last = [], 0, a0
@@ -542,6 +553,7 @@ def main(argv=None):
     # (bookkeeping after the clock stops: none of it inside the timed region)
     host_cpu_s = time.process_time() - cpu0
     threads_cpu = thread_cpu_delta(thr0, thread_cpu(), host_cpu_s)
+    host_samples = sampler.stop() if sampler is not None else None
     retry_delta = [float(ctr1.get(k, 0) - ctr0.get(k, 0)) for k in RETRY_KEYS]
     if rank == 0:
         print(f"[timed] {steps_done} windows decisions={decisions} elapsed={elapsed:.2f}s", file=sys.stderr,
@@ -636,6 +648,7 @@ def main(argv=None):
                        "host": {"cpu_s_all_ranks": round(host_cpu_s, 1),
                                 # rank 0's CPU seconds by thread group over the timed region
                                 "cpu_s_by_thread_rank0": threads_cpu,
+                                **({"samples_rank0": host_samples} if host_samples else {}),
                                 "threads_per_rank": host_threads,
                                 "rayon_threads": os.environ.get("RAYON_NUM_THREADS"),
                                 "cpu_s_per_decision": (round(host_cpu_s / total_decisions, 4)
