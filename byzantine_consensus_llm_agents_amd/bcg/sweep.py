@@ -183,6 +183,8 @@ def summarize(games: List[Dict], elapsed: float, n_gpus: int) -> Dict:
 
 def main(argv=None) -> Dict:
     args = build_parser().parse_args(argv)
+    from ..utils.threads import rank_thread_budget
+    rank_thread_budget(int(os.environ.get("WORLD_SIZE", "1")))  # before torch / tokenizer pools start
     saved_stdout, sys.stdout = sys.stdout, sys.stderr  # agents' console messages; the summary line stays alone
     try:
         return _main(args)
