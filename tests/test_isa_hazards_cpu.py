@@ -5,8 +5,8 @@ Three regressions this catches (each seen once while building the persistent fou
 
 * a VALU write of an MFMA source register right before the asm MFMA (the zero-operand MFMAs
   that reset the accumulators between items read stale registers: every second item NaN);
-* scratch in a W4 kernel (an accumulator copy outside asm operands re-classed the
-  accumulators and spilled ~300 registers);
+* scratch in a W4 K-loop (an accumulator copy outside asm operands re-classed the
+  accumulators and spilled ~300 registers); the split-K tails after the loop may spill a little;
 * a counter wait other than the ring's own ``vmcnt(8)`` inside the W4 K-loop (an epilogue load
   left pending across the loop's back edge made hipcc put ``vmcnt(0)`` at the top of every
   K-tile, draining the LDS-DMA pieces in flight).
@@ -93,7 +93,6 @@ def test_w4_kernels_spill_free_and_k_loop_waits_only_for_the_ring(asm):
     assert len(kernels) == 5  # bf16 store / SiLU / residual, fp8 store / residual
     for k, body in kernels:
         lines = [ln.strip() for ln in body.split("\n")]
-        assert not [ln for ln in lines if ln.startswith("scratch_")], k
         blocks, cur = [], []
         for ln in lines:
             if re.match(r"^(\.LBB\d+_\d+:|; %bb\.\d+:)", ln):
@@ -105,5 +104,12 @@ def test_w4_kernels_spill_free_and_k_loop_waits_only_for_the_ring(asm):
                        and any("s_barrier" in x for x in b)]
         assert loop_blocks, k
         for b in loop_blocks:
+            # the K-loop never touches scratch (the split-K / stream-K tails after it may: their
+            # fp32 sums and epilogue share the register file with the 256 accumulators)
+            assert not [x for x in b if x.startswith("scratch_")], k
             waits = [x for x in b if x.startswith("s_waitcnt") and "vmcnt" in x]
             assert all("vmcnt(8)" in x for x in waits), (k, waits)
+        # and the tails' spill area stays small
+        m = re.search(r"\.amdhsa_kernel " + re.escape(k) + r"\n.*?\.amdhsa_private_segment_fixed_size (\d+)",
+                      text, re.S)
+        assert m and int(m.group(1)) <= 2048, (k, m and m.group(1))
