@@ -103,14 +103,6 @@
 #ifndef W4_NT_STORE
 #define W4_NT_STORE 0  // non-temporal output stores; measured: 3-6 % slower
 #endif
-// reduce-scatter split-K arrival counters: 2 ints per tile from this index of the counter array
-#define W4_RS_CNT0 65024
-#ifndef W4_ACC_SETTLE
-#define W4_ACC_SETTLE 0  // split-K tails start with acc_settle() (measured: broke the tail's numbers)
-#endif
-#ifndef W4_RS_SPLIT
-#define W4_RS_SPLIT 0  // split-K reduce-scatter when every workgroup is resident (see the tail)
-#endif
 #ifndef W4_PERSIST
 #define W4_PERSIST 1  // one workgroup per CU streaming its tiles (split_k == 1; profiles/r4_gemm_w4)
 #endif
@@ -200,7 +192,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     const void* __restrict__ Xv, const void* __restrict__ Wv, const bf16_t* __restrict__ bias,
     const bf16_t* __restrict__ residual, bf16_t* __restrict__ C, float* __restrict__ ws,
     int* __restrict__ counters, int M, int N, int K, int ldc, int inter, int m_tiles, int n_tiles,
-    int split_k, int rs_split, const float* __restrict__ x_scale, const float* __restrict__ w_scale) {
+    int split_k, const float* __restrict__ x_scale, const float* __restrict__ w_scale) {
   static_assert(!F8 || (EPI != EPI_SILU_MUL && !M32), "fp8: store / residual epilogues");
   constexpr bool L32 = M32 || F8;                      // 32x32 accumulator layout
   constexpr int SLOTS = F8 ? 16 : W4_SLOTS;            // MFMAs per phase
@@ -228,7 +220,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   // logical workgroup r (XCD-grouped: the workgroups of one XCD own one contiguous eighth of
   // the units) streams range r -- a partial first tile, whole tiles, a partial last tile.
   // Whole tiles take the ordinary in-stream epilogue; a partial segment stores its fp32 part
-  // (per wave, write-through) and the workgroup that arrives last for that tile adds every
+  // (per wave, write-through) and the wave that arrives last for that (tile, wave) adds every
   // segment's part after its stream and runs the epilogue -- nobody waits on another workgroup.
   // The tile quantisation of decode-size M goes away (gate_up at 704 rows: 408 tiles = 1.6 per
   // CU instead of two rounds).
@@ -453,7 +445,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   //   32x32x16: block (nb, mb) lane: D[n = 32 nb + 8 g + 4 (lane >> 5) + e][m = 32 mb + (lane & 31)],
   //             registers 4 g + e;  i = 4 nb + g (g = 0..3)
   // value(nb, mb) returns the block's registers (accumulators, or the split-K slab sum).
-  auto epilogue = [&](const Geo& geo_c, auto value, uint32_t stage = 0xffffffffu, uint32_t jmask = 0xffu) {
+  auto epilogue = [&](const Geo& geo_c, auto value, uint32_t stage = 0xffffffffu) {
     constexpr int MB = L32 ? 32 : 16;
     constexpr int NG = L32 ? 4 : 1;  // quads per block
     // the lane index re-enters here through an opaque move: the epilogue's per-lane address
@@ -547,7 +539,6 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       if constexpr (SILU) {
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
-          if (!((jmask >> j) & 1)) continue;  // (an m-block another split stores)
 #pragma unroll
           for (int p = 0; p < NP; ++p) {
             // 16-row blocks of the tile alternate gate / up of the same 16 features: output quad
@@ -594,13 +585,11 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 #pragma unroll
             for (int p = 0; p < NP; ++p) bq[p] = __builtin_amdgcn_raw_buffer_load_b128(rb, colv[p], 0, 0);
           }
-          static_assert(JG == 1, "the m-block mask is per batch");
-          if (jmask & 1) load_rq(0, 0);
+          load_rq(0, 0);
 #pragma unroll
           for (int j0 = 0; j0 < NB; j0 += JG) {
             const int bf = (j0 / JG) & 1;
-            if (j0 + JG < NB && ((jmask >> (j0 + JG)) & 1)) load_rq(bf ^ 1, j0 + JG);
-            if (!((jmask >> j0) & 1)) continue;  // (an m-block another split stores)
+            if (j0 + JG < NB) load_rq(bf ^ 1, j0 + JG);
 #pragma unroll
             for (int jj = 0; jj < JG; ++jj)
 #pragma unroll
@@ -802,22 +791,6 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     }
   };
 
-  // split-K tails: one zero-operand builtin MFMA per accumulator block first.  hipcc does not
-  // know an asm statement is an MFMA; after these it does -- every later read of the
-  // accumulators gets its wait states from hipcc itself, and its register allocation of the
-  // tail spills less (1268 -> ~500 B of scratch for the store epilogue).  ~1k cycles per tail.
-  auto acc_settle = [&]() {
-    const bf16x8 z = {};
-#pragma unroll
-    for (int i = 0; i < NB; ++i)
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        if constexpr (L32)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(z, z, acc[i][j], 0, 0, 0);
-        else
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(z, z, acc[i][j], 0, 0, 0);
-      }
-  };
   // accumulator block -> VGPRs through explicit reads: the accumulators then have no use outside
   // asm AGPR operands inside the loop (a plain copy there lets hipcc re-class them and spill)
   auto read_acc = [&](const auto& a) {
@@ -871,7 +844,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       for (int q = 0; q < 16; ++q) {
         const uint32_t soff = __builtin_amdgcn_readfirstlane(base + q * 1024);
         const uint32_t m0v = __builtin_amdgcn_readfirstlane(lds_w + b * 65536 + q * 1024);
-        asm volatile("s_mov_b32 m0, %3\n\tbuffer_load_dwordx4 %0, %1, %2 offen sc1 lds"
+        asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen sc1 lds"
                      :
                      : "v"(static_cast<uint32_t>(lane) * 16), "s"(srd), "s"(soff), "s"(m0v)
                      : "memory", "m0");
@@ -882,13 +855,11 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       for (int q = 0; q < 16; ++q) {
         const int f = 16 * g + q, i = f / (NB * QPB), j = (f / QPB) % NB, qq = f % QPB;
         const f32x4 v = *reinterpret_cast<const f32x4*>(smem + wave * 16384 + b * 65536 + q * 1024 + lane * 16);
-        // plain arithmetic: past the K-loop hipcc moves accumulators between AGPRs and VGPRs
-        // under pressure, and its AGPR write right before an asm read of that AGPR gets no
-        // wait states (asm reads here returned stale elements: one element of one block, in
-        // some launches)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float a;
+          // (s_nop 1: out here hipcc moves accumulators through AGPRs under pressure, and its
+          // AGPR write right before this read gets no wait states from it)
           asm volatile("s_nop 1\n\tv_accvgpr_read_b32 %0, %1" : "=v"(a) : "a"(acc[i][j][4 * qq + e]));
           a += v[e];
           asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(acc[i][j][4 * qq + e]) : "v"(a));
@@ -909,14 +880,14 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
           asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // this round landed, the next in flight
         else
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // (the bytes of an LDS-DMA can land after its vmcnt: a barrier before the reads, as in
-        // the reduce-scatter rounds -- every wave of the workgroup runs add_parts)
-#ifndef W4_NO_PARTS_BAR
+        // the bytes of an LDS-DMA can land after its vmcnt has retired (measured: an element
+        // of a piece read stale, vmcnt(0) included): vmcnt, then a barrier, then the reads
+        // (cdna_hip_programming.md).  Every wave of the workgroup runs add_parts.
         asm volatile("s_barrier" ::: "memory");
-#endif
         consume(g, g & 1);
       }
     }
+    asm volatile("s_nop 4" ::: "memory");  // (AGPR writes -> the epilogue's reads)
   };
   // stream-K: the logical workgroup whose range holds unit u; the tile's segments are those of
   // workgroups wg_of(T nk) .. wg_of((T + 1) nk - 1), segment (r, T) stored in part 2 r + (T is
@@ -1037,16 +1008,12 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       }
 #endif
       phase_b(t, ktd, sX, sW, sch);
-      // the MFMA D -> read wait states at the end of every K-tile, inside the loop: whatever
-      // hipcc then does with the accumulators -- the item-end block's reads, its register
-      // shuffles on the loop exit (a copy of a just-written block there read 16-lane rows not
-      // yet written) -- comes after them.  (The wave waits here for the MFMA pipe it would wait
-      // for at the next phase's barrier anyway.)
-#if W4_NOP_LAST
-      if (t == total - 1 || (nsplit == 1 && ktc + 1 == gc.nk)) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
-#else
+      // the MFMA D -> read wait states at the end of every K-tile, inside the loop: hipcc does
+      // not know an asm statement is an MFMA, so whatever it then does with the accumulators --
+      // the item-end block's reads, its register shuffles on the loop exit (a copy of a
+      // just-written block there read 16-lane rows not yet written) -- must come after these.
+      // (The wave waits for the MFMA pipe here instead of at the next phase's barrier.)
       asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
-#endif
 #ifdef W4_STAMPS
       t_end = __builtin_amdgcn_s_memtime();
       cyc_b += t_end - t_w;
@@ -1110,21 +1077,15 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         const Geo gp = geo(j);
         if (gp.nk == nk_all) return;  // a whole tile: its epilogue ran in the stream
         const int T = gp.tile;
-        // every wave's part of T is stored (sc1, drained before the stream's end); the
-        // workgroup that counts last over the tile's segments sums them -- one decision per
-        // workgroup, so add_parts' barriers see all four waves
-        __syncthreads();
-        int* flag = reinterpret_cast<int*>(smem);
-        if (tid == 0) {
-          int* cnt = counters + T;
-          const int last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nseg(T) - 1;
+        // this wave's part of T is stored (sc1, drained); the wave that counts last for (T,
+        // wave) over the tile's segments sums them
+        int last = 0;
+        if (lane == 0) {
+          int* cnt = counters + T * 4 + wave;
+          last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nseg(T) - 1;
           if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          flag[0] = last;
         }
-        __syncthreads();
-        const int last = flag[0];
-        __syncthreads();  // every wave has read the flag before the part rounds overwrite it
-        if (!last) return;
+        if (!__builtin_amdgcn_readlane(last, 0)) return;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         // zeros by VALU writes, not zero_acc's MFMAs: out here hipcc spills and reloads
         // accumulators between the asm statements, and its spill store of an asm MFMA's result
@@ -1141,7 +1102,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         Geo g;
         g.tile = T;
         tile_geo(g);
-        epilogue(g, [&](int i, int jj) { return acc[i][jj]; });
+        epilogue(g, [&](int i, int jj) { return read_acc_tail(acc[i][jj]); });
       };
       if (n_items > 0) reduce_item(0);
       if (n_items > 1) reduce_item(n_items - 1);
@@ -1149,12 +1110,6 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     return;
   }
   if (split_k == 1) return;  // (the epilogues ran in the stream)
-#if W4_ABL_TAIL == 1  // timing ablation: no split-K tail at all (wrong results)
-  return;
-#endif
-#if W4_ACC_SETTLE
-  acc_settle();
-#endif
 
   // ---- split-K (one item per workgroup): every split stores its fp32 tile write-through (sc1);
   // the last arriver adds the OTHER splits' slabs into its own accumulators and runs the
@@ -1172,114 +1127,6 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   auto slab_off = [&](int sp, int i, int j, int qq) {
     return (sp * (BM * BN) + (((wave * NB + i) * NB + j) * QPB + qq) * 256 + lane * 4) * 4;
   };
-  if constexpr (!L32) {
-    if (rs_split) {
-      // ---- reduce-scatter split-K (every workgroup of the launch resident: one per CU, the
-      // host checks nwg <= CUs).  Split s owns m-blocks [jlo, jhi) of every wave's quadrant:
-      // it stores the other m-blocks' fp32 pieces (write-through), waits until all S splits of
-      // the tile have stored, adds the S - 1 other splits' pieces of its own m-blocks and runs
-      // the epilogue on those rows only.  Against the last-arriver scheme: (S-1)/S of a slab
-      // stored instead of all of it, (S-1)/S of one slab read per workgroup instead of S - 1
-      // whole slabs by one, and the epilogue spread over S CUs (qkv at 704 rows: the tail was
-      // 30 of 71 us).
-      const int S = split_k, sp0 = gc.split;
-      const int jlo = sp0 * NB / S, jhi = (sp0 + 1) * NB / S;
-#pragma unroll
-      for (int i = 0; i < NB; ++i)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          if (j >= jlo && j < jhi) continue;
-          const f32x4 part = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, part), rs, slab_off(sp0, i, j, 0), 0,
-                                                 16 /*sc1*/);
-        }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      // arrival: cnt counts the tile's stored splits (the last resets it), gen is bumped by the
-      // last and waited on by the others -- both left consistent for the next launch.  Their
-      // slots sit at the top of the counter array, clear of every other scheme's.
-      if (tid == 0) {
-        int* cnt = counters + W4_RS_CNT0 + 2 * gc.tile;
-        int* gen = cnt + 1;
-        // (reads of gen are read-modify-writes, performed where every XCD's are: a plain
-        // device-scope load -- what hipcc makes of fetch_add(gen, 0) -- can return this XCD's
-        // stale copy, and a workgroup then reads the other splits' pieces before they are
-        // stored.  An opaque zero keeps the RMW.  The wait is bounded, so a broken invariant
-        // shows as wrong numbers in the tests, not as a hung GPU.)
-        int zero = 0;
-        asm volatile("" : "+v"(zero));
-        const int g0 = __hip_atomic_fetch_add(gen, zero, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == S - 1) {
-          __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_fetch_add(gen, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-          for (int spin = 0; spin < (1 << 22); ++spin) {
-            if (__hip_atomic_fetch_add(gen, zero, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != g0) break;
-            __builtin_amdgcn_s_sleep(2);
-          }
-        }
-      }
-      __syncthreads();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (and every piece load is sc1)
-      // rounds r = 0 .. R-1 of 8 pieces (one m-block j, one other split, the 8 n-blocks) per
-      // wave, 4 buffers of 8 KiB per wave, 3 rounds in flight while one is added
-      const int S1 = S - 1, R = (jhi - jlo) * S1;
-      const i32x4 srd = make_srd(slab, static_cast<uint32_t>(S) * BM * BN * 4);
-      const uint32_t lds_w = lds_base + static_cast<uint32_t>(wave) * 32768;
-      auto issue = [&](int r) {
-        const int j = jlo + r / S1, kk = r % S1, sp = kk < sp0 ? kk : kk + 1;
-#pragma unroll
-        for (int i = 0; i < NB; ++i) {
-          const uint32_t soff = __builtin_amdgcn_readfirstlane(
-              static_cast<uint32_t>(sp * (BM * BN) + ((wave * NB + i) * NB + j) * 256) * 4);
-          const uint32_t m0v = __builtin_amdgcn_readfirstlane(lds_w + (r & 3) * 8192 + i * 1024);
-          asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen sc1 lds"
-                       :
-                       : "v"(static_cast<uint32_t>(lane) * 16), "s"(srd), "s"(soff), "s"(m0v)
-                       : "memory", "m0");
-        }
-      };
-#ifndef W4_RS_DEPTH
-#define W4_RS_DEPTH 3
-#endif
-      constexpr int DEP = W4_RS_DEPTH;
-      for (int r = 0; r < DEP && r < R; ++r) issue(r);
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        if (j < jlo || j >= jhi) continue;
-        for (int kk = 0; kk < S1; ++kk) {
-          const int r = (j - jlo) * S1 + kk;
-          if (r + DEP < R) issue(r + DEP);
-          const int later = min(R - 1 - r, DEP);  // rounds issued after r
-          if (later == 3)
-            asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-          else if (later == 2)
-            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-          else if (later == 1)
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-          else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          // an LDS-DMA's bytes can land in LDS after its vmcnt has retired (measured: one
-          // element of one piece read stale, vmcnt(0) included); the barrier closes that window
-          // (cdna_hip_programming.md: vmcnt, then a barrier, then the ds_read).  Every wave of
-          // the workgroup runs the same R rounds.
-          asm volatile("s_barrier" ::: "memory");
-#pragma unroll
-          for (int i = 0; i < NB; ++i) {
-            acc[i][j] += *reinterpret_cast<const f32x4*>(smem + wave * 32768 + (r & 3) * 8192 + i * 1024 + lane * 16);
-          }
-          // these reads are done before round r + 4 refills buffer r & 3
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-      }
-      uint32_t own = 0;
-#pragma unroll
-      for (int j = 0; j < NB; ++j) own |= (j >= jlo && j < jhi ? 1u : 0u) << j;
-      epilogue(gc, [&](int i, int j) { return acc[i][j]; }, 0xffffffffu, own);
-      return;
-    }
-  }
 #pragma unroll
   for (int i = 0; i < NB; ++i)
 #pragma unroll
@@ -1320,16 +1167,10 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (and every slab load is sc1)
-#if W4_ABL_TAIL == 2  // timing ablation: slabs stored, none read back (wrong results)
-  if (split_k > 0) {
-    epilogue(gc, [&](int i, int j) { return read_acc(acc[i][j]); });
-    return;
-  }
-#endif
   add_parts(slab, static_cast<uint32_t>(split_k) * BM * BN * 4, split_k - 1, [&](int k) {  // the other splits
     return static_cast<uint32_t>(k < gc.split ? k : k + 1) * (BM * BN * 4);
   });
-  epilogue(gc, [&](int i, int j) { return acc[i][j]; });
+  epilogue(gc, [&](int i, int j) { return read_acc(acc[i][j]); });
 }
 
 // compute units of the current device (one resident workgroup each: 160 KiB of LDS)
@@ -1356,12 +1197,9 @@ int launch_w4(const void* x, const void* w, const void* bias, const void* res, v
   // tiles x K-tiles units (split_k == 0, stream-K)
   const int grid = split_k == 0 ? w4_sk_grid(m_tiles * n_tiles, K / (F8 ? 128 : BK))
                    : W4_PERSIST && split_k == 1 ? std::min(nwg, w4_cus()) : nwg;
-  // split-K with every workgroup resident (one per CU): the splits reduce-scatter the tile
-  // (W4_RS_SPLIT, bf16 layout only); otherwise the last arriver sums it
-  const int rs_split = W4_RS_SPLIT && !F8 && !W4_MFMA32 && split_k > 1 && nwg <= w4_cus() ? 1 : 0;
   hipLaunchKernelGGL((gemm_w4_kernel<EPI, !F8 && W4_MFMA32 != 0, F8>), dim3(grid), dim3(256),
                      0, stream, x, w, static_cast<const bf16_t*>(bias), static_cast<const bf16_t*>(res),
-                     static_cast<bf16_t*>(c), ws, cnt, M, N, K, ldc, inter, m_tiles, n_tiles, split_k, rs_split, xs, wsc);
+                     static_cast<bf16_t*>(c), ws, cnt, M, N, K, ldc, inter, m_tiles, n_tiles, split_k, xs, wsc);
   return BCG_CHECK_LAUNCH();
 }
 
@@ -1377,11 +1215,9 @@ BCG_API int bcg_gemm_w4_stamps(void* host, int n) {
 // Same contract as bcg_gemm_pp: epi 0 = store (+bias), 1 = silu(gate)*up into [M, inter],
 // 2 = residual + acc.  K % 64 == 0, K/64 >= split_k; N % 16 == 0 (a partial last n-tile is
 // masked); EPI 1: N == 2*inter, inter % 128 == 0.  split_k > 1: `ws` >= m_tiles*n_tiles*
-// split_k*65536 floats, `counters` = 65536 ints, zeroed before first use (the last-arriver
-// scheme uses [0, tiles) and leaves them zeroed; the reduce-scatter one, [65024, 65536) and
-// leaves them consistent).
+// split_k*65536 floats, `counters` >= m_tiles*n_tiles zeroed ints (left zeroed).
 // split_k == 0: stream-K (one workgroup per CU over the tiles x K-tiles units): `ws` >=
-// bcg_gemm_w4_sk_ws_floats() floats, `counters` >= m_tiles*n_tiles zeroed ints (left zeroed).
+// bcg_gemm_w4_sk_ws_floats() floats, `counters` >= 4*m_tiles*n_tiles zeroed ints (left zeroed).
 BCG_API int bcg_gemm_w4_sk_ws_floats() { return 2 * w4_cus() * BM * BN; }
 
 BCG_API int bcg_gemm_w4(int epi, const void* x, const void* w, const void* bias, const void* residual, void* c,
@@ -1392,11 +1228,10 @@ BCG_API int bcg_gemm_w4(int epi, const void* x, const void* w, const void* bias,
   // the output (and residual) offsets, a masked column's 0x80000000 bias included, stay 32-bit
   if (2ull * (M + BM) * (epi == EPI_SILU_MUL ? inter : N) >= (1ull << 31)) return -2;
   if (split_k != 1 && (!ws || !counters)) return -2;
-  if (split_k == 0) {  // stream-K: a counter per tile; the kernel's unit arithmetic is 32-bit
+  if (split_k == 0) {  // stream-K: 4 counters per tile; the kernel's unit arithmetic is 32-bit
     const long long tiles = 1ll * ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-    if (tiles > W4_RS_CNT0 || tiles * (K / BK) * w4_cus() >= (1ll << 31)) return -2;
+    if (4 * tiles > (1 << 16) || tiles * (K / BK) * w4_cus() >= (1ll << 31)) return -2;
   }
-  if (split_k > 1 && 1ll * ((M + BM - 1) / BM) * ((N + BN - 1) / BN) > W4_RS_CNT0) return -2;
   float* wsf = static_cast<float*>(ws);
   int* cnt = static_cast<int*>(counters);
   switch (epi) {
