@@ -36,7 +36,13 @@ max_tokens (300 decide / 200 vote) -- a pessimistic decode length -- and its
 validity-aware form (every property emitted, >= 10 visible characters per
 free-text field) makes them pass the simulator's validity rules, as a trained
 model's outputs do; ``--plain-grammar`` drops that (a random model then sends
-~30 % of its outputs down the retry ladder: ``detail.retry``).
+~30 % of its outputs down the retry ladder: ``detail.retry``).  Free text is
+printable ASCII (``--unicode-text`` lifts that): a random model's escapes and
+multi-byte characters re-tokenise at several tokens per character once later
+prompts quote them, and late-game prompts then hit the context limit, far
+outside the reference's bounded prompt sizes.  ``detail.prompt_tokens``
+(p50/p95/max per phase) and ``detail.context`` (prompts rejected or cut at the
+context limit) report the envelope the timed region actually saw.
 
 Deadline guard: if the run would pass ``--deadline-s`` (from process start),
 the timed loop stops early and the JSON line reports the windows actually
@@ -103,6 +109,10 @@ def parse(argv=None):
     ap.add_argument("--plain-grammar", action="store_true",
                     help="the reference's schemas as given (no validity-aware bench grammar): a random model "
                          "then closes strings early / skips optional fields and ~30 %% of its outputs retry")
+    ap.add_argument("--unicode-text", action="store_true",
+                    help="free text may hold escapes and multi-byte UTF-8 (default: printable ASCII, as an "
+                         "English-speaking trained model writes; a random model's unicode re-tokenises at "
+                         "several tokens per character and late-game prompts reach the context limit)")
     ap.add_argument("--no-custom-allreduce", action="store_true",
                     help="TP collectives through RCCL only (no xGMI one-/two-shot kernels)")
     ap.add_argument("--kv-cache-gb", type=float, default=None,
@@ -305,7 +315,18 @@ def retry_summary(delta: dict) -> dict:
     rows = out["batch_rows"] + out["sequential_attempts"]
     out["retry_rows"] = rows - prompts
     out["engine_rows_per_prompt"] = round(rows / prompts, 4) if prompts else None
+    exhausted = out["decisions_exhausted"] + out["votes_exhausted"]
+    out["exhausted_pct"] = round(100.0 * exhausted / prompts, 2) if prompts else None
     return out
+
+
+def percentiles(values) -> dict:
+    """n / p50 / p95 / max of a list of prompt lengths (tokens)."""
+    if not values:
+        return {"n": 0}
+    v = sorted(values)
+    pick = lambda q: v[min(len(v) - 1, int(q * (len(v) - 1) + 0.5))]  # noqa: E731
+    return {"n": len(v), "p50": pick(0.50), "p95": pick(0.95), "max": v[-1]}
 
 
 def thread_cpu():
@@ -421,6 +442,7 @@ def main(argv=None):
     C.VLLM_CONFIG["quantization"] = args.quantization
     C.ENGINE_CONFIG.update(backend=args.backend, budget_aware_json=True, seed=args.seed + replica,
                            validity_aware_json=0 if args.plain_grammar else VALIDITY_MIN_VISIBLE,
+                           ascii_text_json=not args.plain_grammar and not args.unicode_text,
                            use_hip_graphs=not args.no_graphs, prefix_caching=not args.no_prefix_cache,
                            custom_allreduce=not args.no_custom_allreduce,
                            kv_cache_dtype=args.kv_cache_dtype)
@@ -496,6 +518,8 @@ def main(argv=None):
 
     eng = getattr(llm.backend, "stats", {})
     stats0 = dict(eng)
+    plens = getattr(llm.backend, "prompt_lens", None)
+    plen0 = {k: len(v) for k, v in plens.items()} if plens is not None else None
     barrier()
     if gpu:
         torch.cuda.synchronize()
@@ -572,6 +596,17 @@ def main(argv=None):
         dist.all_reduce(rt, op=dist.ReduceOp.SUM, group=ctrl)
         retry_delta = rt.tolist()
     retry = retry_summary(dict(zip(RETRY_KEYS, retry_delta)))
+    # prompt sizes of the timed region per phase (the engine records them by requested max_tokens)
+    phase_of = {C.LLM_CONFIG["max_tokens_decide"]: "decide", C.LLM_CONFIG["max_tokens_vote"]: "vote"}
+    prompt_tokens = None
+    if plens is not None:
+        prompt_tokens = {}
+        for mt, lens in list(plens.items()):
+            name = phase_of.get(mt, f"max_tokens_{mt}")
+            prompt_tokens.setdefault(name, []).extend(lens[plen0.get(mt, 0):])
+        prompt_tokens = {k: percentiles(v) for k, v in sorted(prompt_tokens.items())}
+    context = {"rejects": int(d_eng.get("context_rejects", 0)), "short": int(d_eng.get("context_short", 0)),
+               "max_model_len": C.VLLM_CONFIG["max_model_len"]}
     # the layout as every rank saw it: which ranks drive a game pool (one per DP replica, its own
     # seeds) and which only execute their TP driver's plans
     me = {"rank": rank, "replica": replica, "driver": pool is not None,
@@ -592,6 +627,11 @@ def main(argv=None):
         dist.all_reduce(mr, op=dist.ReduceOp.MIN, group=ctrl)
         per_rank_rate = float(mr[0])
     stats = window_stats(per_window, args.window_s)
+    tp_status = getattr(getattr(llm.backend, "tp", None), "custom_status", "off") if args.tp > 1 else "off"
+    if world > 1:  # every group agrees on its own status; rank 0 reports the first fallback, if any
+        statuses = [None] * world
+        dist.all_gather_object(statuses, tp_status, group=ctrl)
+        tp_status = next((s for s in statuses if s.startswith("fallback")), statuses[0])
     if rank == 0:
         line = {
             "metric": f"agent decisions/sec (node), {args.honest}h+{args.byzantine}b BCG {model.split('/')[-1]}; "
@@ -604,7 +644,8 @@ def main(argv=None):
             "kv_cache_dtype": "fp8" if args.kv_cache_dtype == "fp8" else "bf16",
             "data": "synthetic (random-init weights, synthetic BPE tokenizer, budget-aware JSON grammar"
                     + ("" if args.plain_grammar else f", validity-aware: every field, >= {VALIDITY_MIN_VISIBLE} "
-                       "visible chars per free-text field") + ")",
+                       "visible chars per free-text field"
+                       + ("" if args.unicode_text else ", printable-ASCII free text")) + ")",
             "config": {"model": model, "honest": args.honest, "byzantine": args.byzantine,
                        "global_batch": args.sims_per_gpu * (args.honest + args.byzantine) * (world // args.tp),
                        "sims_per_gpu": args.sims_per_gpu, "seq_len": C.VLLM_CONFIG["max_model_len"],
@@ -614,10 +655,13 @@ def main(argv=None):
                        "max_rounds": args.max_rounds, "age_p": args.age_p,
                        "step": f"{args.window_s:g} s window of the continuously-batched pool",
                        "parallelism": f"dp{world // args.tp}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
-                       "hip_graphs": not args.no_graphs, "prefix_caching": not args.no_prefix_cache,
+                       "hip_graphs": not args.no_graphs and getattr(llm.backend, "graphs_off_reason", None) is None,
+                       "prefix_caching": not args.no_prefix_cache,
                        "grammar": "budget-aware" + ("" if args.plain_grammar else
-                                                    f" + validity-aware({VALIDITY_MIN_VISIBLE})"),
-                       "custom_allreduce": args.tp > 1 and not args.no_custom_allreduce},
+                                                    f" + validity-aware({VALIDITY_MIN_VISIBLE})"
+                                                    + ("" if args.unicode_text else " + ascii-text")),
+                       # "on" (xGMI kernels, cross-checked at init), "off", or "fallback:<reason>"
+                       "custom_allreduce": tp_status},
             "detail": {"decisions": total_decisions, "elapsed_s": round(elapsed, 3), "init_s": round(init_s, 1),
                        "steps_requested": args.steps, "window_s": args.window_s,
                        "decisions_per_window_rank0": per_window,
@@ -630,6 +674,7 @@ def main(argv=None):
                        # series A/B comparisons should use
                        "token_window_stats_rank0": window_stats(tok_windows, args.window_s),
                        "retry": retry,
+                       "prompt_tokens_rank0": prompt_tokens, "context_rank0": context,
                        "ranks": ranks,
                        "host": {"cpu_s_all_ranks": round(host_cpu_s, 1),
                                 # rank 0's CPU seconds by thread group over the timed region

@@ -90,6 +90,7 @@ ENGINE_CONFIG = {
     # least this many visible characters (the simulator's validity rules then hold, as for a
     # trained model's outputs); 0 = the reference's schemas as given
     "validity_aware_json": 0,
+    "ascii_text_json": False,
     "max_whitespace": 4,           # JSON grammar: max consecutive whitespace chars
     "prefix_caching": True,
     "use_hip_graphs": True,

@@ -8,8 +8,10 @@ prompts ``:924-1063``, retry suffixes ``:749-759, :846-854, :1262-1272,
 :1366-1374``, schemas ``:590-599, :651-658, :1084-1092, :1155-1162``.
 
 Templates are ``str.format`` strings; every literal brace is doubled.
-Golden renders of the reference live in ``tests/golden/prompts_*.json`` and
-``tests/test_prompts_parity.py`` checks them byte for byte.
+The reference's own prompts, recorded from its unmodified modules driven by
+the scripted engine, live in ``tests/golden/ref_*.json``;
+``tests/test_parity_reference.py`` compares every prompt we send with them
+byte for byte.
 """
 
 from typing import Dict, List, Optional, Tuple

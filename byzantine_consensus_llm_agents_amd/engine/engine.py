@@ -83,6 +83,8 @@ class EngineArgs:
     # benchmark grammar for untrained weights: every property emitted, free-text strings with
     # >= this many visible characters (guided/json_schema.py validity_aware); 0 = the schema as given
     validity_aware_json: int = 0
+    # ... and its free text printable ASCII (late-game prompts stay in the reference's bounded sizes)
+    ascii_text_json: bool = False
     max_whitespace: int = 4
     prefix_caching: bool = True
     use_hip_graphs: bool = True
@@ -126,6 +128,7 @@ class EngineArgs:
                    prefill_chunk_tokens=ec.get("prefill_chunk_tokens", 16384),
                    budget_aware_json=ec.get("budget_aware_json", False),
                    validity_aware_json=int(ec.get("validity_aware_json", 0)),
+                   ascii_text_json=bool(ec.get("ascii_text_json", False)),
                    max_whitespace=ec.get("max_whitespace", 4),
                    prefix_caching=ec.get("prefix_caching", True),
                    use_hip_graphs=ec.get("use_hip_graphs", True),
@@ -156,6 +159,7 @@ class _Seq:
     cached: int = 0
     done_pos: int = 0               # prompt tokens whose KV is written (prefix cache + prefilled chunks)
     error: Optional[str] = None
+    max_new_requested: int = 0      # the caller's max_tokens (before the context-room clamp)
 
 
 class InferenceEngine:
@@ -164,7 +168,17 @@ class InferenceEngine:
         self.timer = PhaseTimer()
         self.stats = {"prompt_tokens": 0, "cached_tokens": 0, "generated_tokens": 0,
                       "decode_steps": 0, "decode_row_steps": 0, "prefill_chunks": 0, "prefill_full_chunks": 0,
-                      "prefill_tail_tokens": 0, "prefill_carried": 0, "calls": 0}
+                      "prefill_tail_tokens": 0, "prefill_carried": 0, "calls": 0,
+                      # prompts with no room for one token (n >= max_model_len): answered "" at once
+                      "context_rejects": 0,
+                      # prompts whose context room cut max_tokens below the grammar's shortest
+                      # complete output (the answer cannot be valid JSON)
+                      "context_short": 0,
+                      # prompts holding lone UTF-16 surrogates (tokenised with U+FFFD in their place)
+                      "prompts_sanitized": 0}
+        # prompt token counts per requested max_tokens (bench.py: decide 300 / vote 200), in
+        # submission order: callers slice them by position for a time window's percentiles
+        self.prompt_lens: Dict[int, List[int]] = collections.defaultdict(list)
         self._carry: List["_Request"] = []  # admitted, prefill incomplete (pending), oldest first
         cfg = args.model_cfg
         self.backend = args.backend
@@ -201,7 +215,8 @@ class InferenceEngine:
         self._req_counter = 0
 
         self.fsm = FSMRegistry(self.tokenizer.all_token_bytes(), cfg.vocab_size, self.device,
-                               max_ws=args.max_whitespace, validity_aware_min=args.validity_aware_json)
+                               max_ws=args.max_whitespace, validity_aware_min=args.validity_aware_json,
+                               ascii_text=args.ascii_text_json)
         self.eos_ids = (self.tokenizer.eos_token_ids + [self.tokenizer.eos_token_ids[0]])[:2]
         self.n_text_tokens = min(self.tokenizer.vocab_size, cfg.vocab_size)
         self._alloc_kv_cache()
@@ -228,7 +243,15 @@ class InferenceEngine:
         self._snap = None        # host copy of (done, gen_count, out_tokens) after the last burst
         self._engine_errors = 0
         self._snap_buf = None
-        if self.backend == "hip" and args.use_hip_graphs:
+        # under TP without the xGMI kernels (not requested, or an agreed fallback at init) every
+        # decode collective is a process-group call: decode runs eagerly -- a collective of the
+        # process group inside a captured HIP graph is a path this build does not test
+        # (BCG_TP_GRAPHS_WITH_PG=1 captures anyway)
+        self.graphs_off_reason = None
+        if (self.backend == "hip" and args.use_hip_graphs and self.tp.size > 1 and self.tp.custom is None
+                and os.environ.get("BCG_TP_GRAPHS_WITH_PG") != "1"):
+            self.graphs_off_reason = f"tp collectives through the process group ({self.tp.custom_status})"
+        if self.backend == "hip" and args.use_hip_graphs and self.graphs_off_reason is None:
             from .graphs import DecodeGraphs
             self.graphs = DecodeGraphs(self)
 
@@ -371,20 +394,26 @@ class InferenceEngine:
 
     def _make_request(self, p_ids: List[int], max_tokens: int, temperature: float,
                       fsm_key: Optional[str]) -> "_Request":
-        seq = _Seq(0, list(p_ids), max(1, int(max_tokens)), float(temperature), fsm_key)
+        seq = _Seq(0, list(p_ids), max(1, int(max_tokens)), float(temperature), fsm_key,
+                   max_new_requested=int(max_tokens))
         req = _Request(seq)
         n, limit = len(p_ids), self.args.max_model_len
         if n == 0 or n >= limit:
+            req.limit = "context_rejects"
             req.finish("")  # no room for even one token: the caller sees an unparsable (empty) output
         else:
             # generate up to the context limit, as vLLM does (not an empty answer)
             seq.max_new = min(seq.max_new, limit - n, OUT_WIDTH)
+            if fsm_key is not None and seq.max_new < int(max_tokens):
+                shortest = int(self.fsm._fsms[fsm_key].dist[0]) if fsm_key in self.fsm._fsms else 0
+                if seq.max_new < shortest:
+                    req.limit = "context_short"
         return req
 
     def submit(self, prompts: List[str], params_list) -> List["_Request"]:
         """Tokenise + compile schemas on the caller's thread (CPU only), hand to the scheduler."""
         with self.timer.phase("tokenize"):
-            ids = self.tokenizer.encode_batch(prompts)
+            ids, sanitized = self.tokenizer.encode_batch_safe(prompts)
         reqs = []
         for p_ids, p in zip(ids, params_list):
             schema = p.guided_decoding.json if p.guided_decoding is not None else None
@@ -393,6 +422,11 @@ class InferenceEngine:
             reqs.append(self._make_request(p_ids, p.max_tokens, p.temperature, key))
         with self._cv:
             self.stats["calls"] += 1
+            self.stats["prompts_sanitized"] += sanitized
+            for r in reqs:
+                self.prompt_lens[r.seq.max_new_requested].append(len(r.seq.prompt_ids))
+                if r.limit:
+                    self.stats[r.limit] += 1
             self._incoming.extend(r for r in reqs if not r.event.is_set())
             self._cv.notify_all()
         return reqs
@@ -964,11 +998,12 @@ class InferenceEngine:
 
 
 class _Request:
-    __slots__ = ("seq", "row", "text", "exc", "event", "pending", "enq_burst")
+    __slots__ = ("seq", "row", "text", "exc", "event", "pending", "enq_burst", "limit")
 
     def __init__(self, seq: _Seq, enq_burst: int = 0):
         self.seq, self.row, self.text, self.exc, self.pending = seq, -1, "", None, False
         self.enq_burst = enq_burst
+        self.limit = None  # the stats counter of a context-limited request
         self.event = threading.Event()
 
     def finish(self, text: str):

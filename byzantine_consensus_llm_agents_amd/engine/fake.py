@@ -260,6 +260,7 @@ class HostModelBackend:
         self.lock = threading.Lock()
         self.free_at = 0.0
         self.stats = {"prompt_tokens": 0, "cached_tokens": 0, "generated_tokens": 0, "calls": 0}
+        self.prompt_lens = {}  # prompt token counts per requested max_tokens (as the real engine)
         self.in_flight = 0
         self.closing = threading.Event()
         self.idle = threading.Condition(self.lock)
@@ -297,6 +298,8 @@ class HostModelBackend:
             self.stats["cached_tokens"] += n_cached
             self.stats["generated_tokens"] += n_gen
             self.stats["calls"] += 1
+            for ids, p in zip(p_ids, params_list):
+                self.prompt_lens.setdefault(int(p.max_tokens), []).append(len(ids))
         delay = done - time.perf_counter()
         if delay > 0:
             time.sleep(delay)

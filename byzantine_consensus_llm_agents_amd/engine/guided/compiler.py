@@ -93,10 +93,11 @@ class FSMRegistry:
     """
 
     def __init__(self, token_bytes: List[bytes], vocab_rows: int, device, max_ws: int = 4,
-                 native: bool = True, validity_aware_min: int = 0):
+                 native: bool = True, validity_aware_min: int = 0, ascii_text: bool = False):
         self.token_bytes = token_bytes
         # > 0: every schema is compiled in its validity-aware form (json_schema.validity_aware)
         self.validity_aware_min = validity_aware_min
+        self.ascii_text = ascii_text  # ... with printable-ASCII free text (json_schema.validity_aware)
         self.vocab_rows = vocab_rows
         self.device = torch.device(device)
         self.max_ws = max_ws
@@ -121,7 +122,7 @@ class FSMRegistry:
     def compile(self, schema: Dict) -> str:
         """CPU compile (any thread); returns the schema key for `install`."""
         if self.validity_aware_min > 0:
-            schema = validity_aware(schema, self.validity_aware_min)
+            schema = validity_aware(schema, self.validity_aware_min, self.ascii_text)
         key = self.key_of(schema)
         if key in self._fsms:  # lock-free hit: entries are published fully built
             return key

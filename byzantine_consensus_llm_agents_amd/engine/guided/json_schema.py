@@ -45,30 +45,45 @@ STRING_CHAR = alt(Cls(byte_mask((0x20, 0x7F)) & ~chars_mask(b'"\\')), *_STRING_C
 # two that need escaping); escapes and non-ASCII characters do not count as visible
 VISIBLE_CHAR = Cls(byte_mask((0x21, 0x7E)) & ~chars_mask(b'"\\'))
 
-# JSON-schema extension keyword of the benchmark's validity-aware grammar: a string carries at
-# least this many visible characters (VISIBLE_CHAR), anywhere in it
+# printable ASCII without the two characters that need escaping: the free text of the benchmark's
+# ASCII grammar (no escapes, no multi-byte UTF-8)
+ASCII_TEXT_CHAR = Cls(byte_mask((0x20, 0x7E)) & ~chars_mask(b'"\\'))
+
+# JSON-schema extension keywords of the benchmark's validity-aware grammar: a string carries at
+# least this many visible characters (VISIBLE_CHAR), anywhere in it; and (ASCII_TEXT) its
+# characters are printable ASCII only
 MIN_VISIBLE = "x-min-visible"
+ASCII_TEXT = "x-ascii-text"
 
 
-def validity_aware(schema: Dict, min_visible: int = 10) -> Dict:
+def validity_aware(schema: Dict, min_visible: int = 10, ascii_text: bool = False) -> Dict:
     """The benchmark grammar for untrained weights (engine option ``validity_aware_json``):
     every object property is emitted (optional ones made required) and every free-text string
     (no enum / const) carries >= `min_visible` visible characters -- the simulator's own validity
     rules for a decision (strategy >= 3, reasoning >= 10 stripped characters, reference
     main.py:232-247) then hold for every output, as they do for a trained model's; a random
     model under the plain grammar closes strings early or skips optional fields, and those
-    outputs go down the retry ladder.  Idempotent (TP followers re-apply it to the key)."""
+    outputs go down the retry ladder.
+
+    `ascii_text`: free text is printable ASCII (no escapes, no multi-byte UTF-8), as an
+    English-speaking trained model writes it.  A random model otherwise emits escapes and
+    multi-byte characters that re-tokenise at several tokens per character once the game
+    quotes them in later prompts (reasoning [:200], strategies 5 x 400 chars), and late-game
+    prompts run into the context limit -- far outside the reference's bounded prompt sizes
+    (~0.6-2.5k tokens).  Idempotent (TP followers re-apply it to the key)."""
     if not isinstance(schema, dict):
         return schema
     out = dict(schema)
     for key in ("anyOf", "oneOf"):
         if key in out:
-            out[key] = [validity_aware(s, min_visible) for s in out[key]]
+            out[key] = [validity_aware(s, min_visible, ascii_text) for s in out[key]]
     if out.get("type") == "object" and "properties" in out:
-        out["properties"] = {k: validity_aware(v, min_visible) for k, v in out["properties"].items()}
+        out["properties"] = {k: validity_aware(v, min_visible, ascii_text) for k, v in out["properties"].items()}
         out["required"] = list(out["properties"])
     if out.get("type") == "string" and "enum" not in out and "const" not in out:
         out[MIN_VISIBLE] = max(int(out.get(MIN_VISIBLE, 0)), min_visible)
+        if ascii_text:
+            out[ASCII_TEXT] = True
     return out
 
 
@@ -145,9 +160,14 @@ class SchemaCompiler:
         if kind == "string" and schema.get(MIN_VISIBLE):
             # (invisible chars* visible){k} then any chars: >= k visible characters
             k = int(schema[MIN_VISIBLE])
-            invisible = alt(Cls(chars_mask(b" \x7f")), *_STRING_CHAR_NON_ASCII)
-            body = seq(Rep(seq(Star(invisible), VISIBLE_CHAR), k, k), Star(STRING_CHAR))
+            if schema.get(ASCII_TEXT):
+                invisible, char = lit(" "), ASCII_TEXT_CHAR
+            else:
+                invisible, char = alt(Cls(chars_mask(b" \x7f")), *_STRING_CHAR_NON_ASCII), STRING_CHAR
+            body = seq(Rep(seq(Star(invisible), VISIBLE_CHAR), k, k), Star(char))
             return seq(lit('"'), body, lit('"'))
+        if kind == "string" and schema.get(ASCII_TEXT) and "enum" not in schema:
+            return seq(lit('"'), Star(ASCII_TEXT_CHAR), lit('"'))
         if kind == "string":
             n = schema.get("maxLength")
             body = Rep(STRING_CHAR, int(schema.get("minLength", 0)), int(n)) if n is not None else (

@@ -142,6 +142,17 @@ class BCGTokenizer:
     def encode_batch(self, texts: List[str]) -> List[List[int]]:
         return [e.ids for e in self.tok.encode_batch(texts, add_special_tokens=False)]
 
+    def encode_batch_safe(self, texts: List[str]):
+        """encode_batch for text that may hold lone UTF-16 surrogates (a JSON ``\\ud83d`` escape
+        json.loads accepts, quoted back into a later prompt): the tokenizer refuses such a string,
+        and with it the whole batch.  Those characters become U+FFFD instead.  Returns (ids, the
+        number of texts that needed it)."""
+        try:
+            return self.encode_batch(texts), 0
+        except (TypeError, ValueError, UnicodeError):
+            fixed = [encodable(t) for t in texts]
+            return self.encode_batch(fixed), sum(a is not b for a, b in zip(fixed, texts))
+
     def decode(self, ids: List[int]) -> str:
         return self.tok.decode(ids, skip_special_tokens=True)
 
@@ -164,6 +175,15 @@ class BCGTokenizer:
 
     def all_token_bytes(self) -> List[bytes]:
         return [self.token_bytes(i) for i in range(self.vocab_size)]
+
+
+def encodable(text: str) -> str:
+    """`text` with every lone surrogate replaced by U+FFFD (the same object when it has none)."""
+    try:
+        text.encode("utf-8")
+        return text
+    except UnicodeEncodeError:
+        return "".join("\ufffd" if 0xD800 <= ord(c) <= 0xDFFF else c for c in text)
 
 
 def family_of(model_name: str) -> str:

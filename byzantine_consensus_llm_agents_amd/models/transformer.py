@@ -57,6 +57,8 @@ class TPGroup:
                  chunk_large: bool = False):
         self.group, self.rank, self.size, self.custom = group, rank, size, custom
         self.ctrl = ctrl        # CPU (gloo) group of the same ranks: the driver's plan broadcasts
+        # "on" (xGMI kernels, cross-checked), "off" (not requested) or "fallback:<reason>"
+        self.custom_status = "on" if custom is not None else "off"
         self.leader = leader    # global rank of this group's rank 0 (the driver)
         self.chunk_large = chunk_large
 

@@ -13,11 +13,38 @@ from types import SimpleNamespace
 
 import torch
 
-from ..utils.build import kernels_target
+from ..utils.build import kernel_sources, kernels_source_hash, kernels_target
 
 _LIB = None
 
 c_int, c_float, c_void_p, c_uint32, c_int64 = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int64
+
+
+class StaleLibraryError(RuntimeError):
+    pass
+
+
+def library_stamp(lib: ctypes.CDLL) -> str:
+    fn = getattr(lib, "bcg_source_hash", None)
+    if fn is None:
+        return None
+    fn.argtypes, fn.restype = [], ctypes.c_char_p
+    return fn().decode()
+
+
+def check_source_stamp(lib: ctypes.CDLL, path: str):
+    """Refuse a library built from other sources than the tree's csrc/kernels.
+
+    ``utils/build.py`` stamps the library with a hash of every kernel source.
+    A deployment without sources (no csrc/kernels) has nothing to compare with
+    and is accepted."""
+    if not kernel_sources()[0]:
+        return
+    want, got = kernels_source_hash(), library_stamp(lib)
+    if got != want:
+        raise StaleLibraryError(
+            f"{path} was built from other sources (stamp {got!r}, csrc/kernels {want!r}); rebuild with "
+            "`python -m byzantine_consensus_llm_agents_amd.utils.build --force`")
 
 
 def load_library(path: str = None) -> ctypes.CDLL:
@@ -29,6 +56,7 @@ def load_library(path: str = None) -> ctypes.CDLL:
         raise RuntimeError(f"HIP kernel library not found at {path}; run `python -m "
                            "byzantine_consensus_llm_agents_amd.utils.build` (hipcc --offload-arch=gfx950)")
     lib = ctypes.CDLL(path)
+    check_source_stamp(lib, path)
     sig = {
         "bcg_add_rmsnorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_int, c_void_p],
         "bcg_silu_mul": [c_void_p, c_void_p, c_int64, c_int, c_void_p],

@@ -275,46 +275,128 @@ def _alloc(lib, cap_bytes: int):
 
 
 class XGMIAllReduce(_Rank):
-    """Custom all-reduce of one TP group (one process per GPU, IPC-mapped peer buffers)."""
+    """Custom all-reduce of one TP group (one process per GPU, IPC-mapped peer buffers).
+
+    The constructor never leaves a peer waiting: a rank whose allocation, handle export or
+    peer mapping fails records why in ``error`` and still takes part in the handle exchange and
+    the closing barrier.  ``establish`` (below) agrees on the outcome over the whole group and
+    falls back to RCCL when any rank failed.  ``fault="ipc"`` injects a mapping failure on the
+    group's last rank (tests of that fallback)."""
 
     def __init__(self, group, cap_bytes: int = DEFAULT_CAP, oneshot_max: int = ONESHOT_MAX,
-                 timeout_s: float = 30.0):
+                 timeout_s: float = 30.0, fault: Optional[str] = None):
         import torch.distributed as dist
-        lib = _lib()
         rank, world = dist.get_rank(group), dist.get_world_size(group)
-        d, s = _alloc(lib, cap_bytes)
-        hsz = lib.bcg_ar_ipc_handle_size()
-        hd, hs = ctypes.create_string_buffer(hsz), ctypes.create_string_buffer(hsz)
-        if lib.bcg_ar_ipc_handle(ctypes.c_void_p(d), hd) or lib.bcg_ar_ipc_handle(ctypes.c_void_p(s), hs):
-            raise RuntimeError("custom all-reduce: hipIpcGetMemHandle failed")
+        self.error: Optional[str] = None
+        self._own, self._opened, self.lib = None, [], None
+        mine = None
+        try:
+            lib = self.lib = _lib()
+            d, s = _alloc(lib, cap_bytes)
+            self._own = (d, s)
+            hsz = lib.bcg_ar_ipc_handle_size()
+            hd, hs = ctypes.create_string_buffer(hsz), ctypes.create_string_buffer(hsz)
+            if lib.bcg_ar_ipc_handle(ctypes.c_void_p(d), hd) or lib.bcg_ar_ipc_handle(ctypes.c_void_p(s), hs):
+                raise RuntimeError("hipIpcGetMemHandle failed")
+            mine = (hd.raw, hs.raw)
+        except Exception as exc:  # noqa: BLE001 -- reported through `error`, agreed by establish()
+            self.error = f"export: {exc}"
         handles = [None] * world
-        dist.all_gather_object(handles, (hd.raw, hs.raw), group=group)
-        data, sig, self._opened = [], [], []
-        for r, (h_d, h_s) in enumerate(handles):
-            if r == rank:
-                data.append(d)
-                sig.append(s)
-                continue
-            pd, ps = ctypes.c_void_p(), ctypes.c_void_p()
-            if (lib.bcg_ar_ipc_open(ctypes.create_string_buffer(h_d, hsz), ctypes.byref(pd))
-                    or lib.bcg_ar_ipc_open(ctypes.create_string_buffer(h_s, hsz), ctypes.byref(ps))):
-                raise RuntimeError(f"custom all-reduce: hipIpcOpenMemHandle of rank {r} failed")
-            data.append(pd.value)
-            sig.append(ps.value)
-            self._opened += [pd.value, ps.value]
-        self._own = (d, s)
-        super().__init__(lib, rank, world, data, sig, cap_bytes, oneshot_max, timeout_s)
-        dist.barrier(group=group)  # every peer mapped before anyone launches
+        dist.all_gather_object(handles, mine, group=group)
+        data, sig = [], []
+        if self.error is None:
+            try:
+                for r, h in enumerate(handles):
+                    if h is None:
+                        raise RuntimeError(f"rank {r} exported no handle")
+                    if r == rank:
+                        data.append(self._own[0])
+                        sig.append(self._own[1])
+                        continue
+                    if fault == "ipc" and rank == world - 1:
+                        raise RuntimeError(f"injected hipIpcOpenMemHandle failure (rank {r}'s buffers)")
+                    pd, ps = ctypes.c_void_p(), ctypes.c_void_p()
+                    if lib.bcg_ar_ipc_open(ctypes.create_string_buffer(h[0], hsz), ctypes.byref(pd)):
+                        raise RuntimeError(f"hipIpcOpenMemHandle of rank {r} failed")
+                    self._opened.append(pd.value)
+                    if lib.bcg_ar_ipc_open(ctypes.create_string_buffer(h[1], hsz), ctypes.byref(ps)):
+                        raise RuntimeError(f"hipIpcOpenMemHandle of rank {r} failed")
+                    self._opened.append(ps.value)
+                    data.append(pd.value)
+                    sig.append(ps.value)
+                super().__init__(lib, rank, world, data, sig, cap_bytes, oneshot_max, timeout_s)
+            except Exception as exc:  # noqa: BLE001
+                self.error = f"ipc: {exc}"
+        dist.barrier(group=group)  # every peer mapped (or failed) before anyone launches
 
     def close(self):
-        if self._own is None:
+        if self._own is None and not self._opened:
             return
         torch.cuda.synchronize()
         for p in self._opened:
             self.lib.bcg_ar_ipc_close(ctypes.c_void_p(p))
-        for p in self._own:
+        for p in self._own or ():
             self.lib.bcg_ar_free(ctypes.c_void_p(p))
         self._own, self._opened = None, []
+
+
+def cross_check(custom, group, device, fault: Optional[str] = None) -> Optional[str]:
+    """One-shot and two-shot all-reduce of a rank-dependent tensor against the process group's
+    own ``dist.all_reduce`` (small integers: exact in bf16, so the results must be bitwise equal).
+    Returns None when both agree, else what differed.  ``fault="mismatch"`` perturbs the custom
+    result on the group's last rank (tests of the fallback).  Every rank runs every collective
+    whatever it found (an early return would leave its peers waiting in the next one)."""
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    found = None
+    for mode, n in ((1, 4096), (2, min(custom.cap_bytes // 2, 1 << 20) // 8 * 8)):
+        x = ((torch.arange(n, device=device) % 7) + rank + 1).to(torch.bfloat16)
+        ref = x.clone()
+        dist.all_reduce(ref, group=group)
+        got = custom.all_reduce_(x.clone(), mode=mode)
+        if fault == "mismatch" and rank == world - 1:
+            got[n // 2] += 1
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        if not torch.equal(got, ref) and found is None:
+            bad = int((got != ref).sum())
+            found = f"mismatch: {'one' if mode == 1 else 'two'}-shot differs from the process group in {bad} of {n}"
+    return found
+
+
+def establish(group, ctrl, make, device, fault: Optional[str] = None):
+    """Bring up a custom all-reduce for `group`, or agree to fall back to the process group.
+
+    ``make(fault)`` constructs it (``XGMIAllReduce``; a stand-in in CPU tests) and must return an
+    object with ``error`` set on any failure of this rank.  The ranks agree over `ctrl` (a CPU
+    group: it still works when the device path is broken) first on construction, then on a
+    ``cross_check`` against ``dist.all_reduce``.  Returns ``(custom or None, status)`` with status
+    ``"on"`` or ``"fallback:<reason>"`` -- identical on every rank of the group."""
+    import torch.distributed as dist
+
+    def agree(reason):
+        reasons = [None] * dist.get_world_size(ctrl)
+        dist.all_gather_object(reasons, reason, group=ctrl)
+        return next((f"rank{r}:{x}" for r, x in enumerate(reasons) if x), None)
+
+    custom, reason = None, None
+    try:
+        custom = make(fault)
+        reason = getattr(custom, "error", None)
+    except Exception as exc:  # noqa: BLE001 -- a rank that cannot even construct still agrees
+        reason = f"init: {exc}"
+    reason = agree(reason)
+    if reason is None:
+        try:
+            local = cross_check(custom, group, device, fault)
+        except Exception as exc:  # noqa: BLE001
+            local = f"cross-check: {exc}"
+        reason = agree(local)
+    if reason is None:
+        return custom, "on"
+    if custom is not None and hasattr(custom, "close"):
+        custom.close()
+    return None, f"fallback:{reason}"
 
 
 class LocalRanks:

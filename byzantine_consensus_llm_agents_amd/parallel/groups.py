@@ -54,6 +54,7 @@ _TP_GROUPS = {}
 _TP_CTRL = {}
 _DP_GROUPS = {}
 _CUSTOM_AR = {}
+_CUSTOM_STATUS = {}
 
 
 def env_layout(tp: int = 1) -> Layout:
@@ -115,24 +116,39 @@ def tensor_parallel_group(tp: int, custom_allreduce: bool = False, hidden: Optio
                 mine, ctrl = pg, cg
         _TP_GROUPS[tp] = mine
         _TP_CTRL[tp] = ctrl
-    custom = None
     mode = os.environ.get("BCG_CUSTOM_AR", "1")  # 0 = RCCL only, force = also over gloo (1-GPU tests)
     if custom_allreduce and mode != "0" and (mode == "force" or dist.get_backend(_TP_GROUPS[tp]) == "nccl"):
-        if tp not in _CUSTOM_AR:
-            from .custom_allreduce import XGMIAllReduce
-            # BCG_AR_CAP_MB: largest message of the xGMI kernels (RCCL above it; over gloo the
-            # larger messages go through the kernels in cap-sized pieces, TPGroup.chunk_large)
-            _CUSTOM_AR[tp] = XGMIAllReduce(_TP_GROUPS[tp], cap_bytes=int(os.environ.get("BCG_AR_CAP_MB", "32")) << 20,
-                                           timeout_s=float(os.environ.get("BCG_AR_TIMEOUT_S", "30")))
-            # routing limits measured on this group's links (RCCL groups; BCG_AR_CALIBRATE=0 keeps the
-            # built-in rule, =force also calibrates over gloo -- one-GPU tests of the mechanism)
-            cal = os.environ.get("BCG_AR_CALIBRATE", "1")
-            if cal == "force" or (cal != "0" and dist.get_backend(_TP_GROUPS[tp]) == "nccl"):
-                _CUSTOM_AR[tp].calibrate(_TP_GROUPS[tp], route=dist.get_backend(_TP_GROUPS[tp]) == "nccl",
-                                         hidden=hidden)
-        custom = _CUSTOM_AR[tp]
-    return TPGroup(_TP_GROUPS[tp], lay.tp_rank, tp, custom=custom, ctrl=_TP_CTRL[tp],
-                   leader=lay.rank - lay.tp_rank, chunk_large=dist.get_backend(_TP_GROUPS[tp]) == "gloo")
+        if tp not in _CUSTOM_STATUS:
+            _CUSTOM_AR[tp], _CUSTOM_STATUS[tp] = _establish_custom(tp, hidden)
+    else:
+        _CUSTOM_STATUS.setdefault(tp, "off")
+    g = TPGroup(_TP_GROUPS[tp], lay.tp_rank, tp, custom=_CUSTOM_AR.get(tp), ctrl=_TP_CTRL[tp],
+                leader=lay.rank - lay.tp_rank, chunk_large=dist.get_backend(_TP_GROUPS[tp]) == "gloo")
+    g.custom_status = _CUSTOM_STATUS[tp]
+    return g
+
+
+def _establish_custom(tp: int, hidden: Optional[int]):
+    """The xGMI all-reduce of this rank's TP group, cross-checked against the process group, or
+    an agreed fallback to it (``custom_allreduce.establish``): a first run on a node whose IPC
+    mapping or peer access fails serves through RCCL instead of dying at TP init.
+    ``BCG_AR_FAULT=ipc|mismatch`` injects either failure (tests)."""
+    from .custom_allreduce import XGMIAllReduce, establish
+    group, ctrl = _TP_GROUPS[tp], _TP_CTRL[tp]
+    fault = os.environ.get("BCG_AR_FAULT") or None
+    # BCG_AR_CAP_MB: largest message of the xGMI kernels (RCCL above it; over gloo the larger
+    # messages go through the kernels in cap-sized pieces, TPGroup.chunk_large)
+    make = lambda f: XGMIAllReduce(group, cap_bytes=int(os.environ.get("BCG_AR_CAP_MB", "32")) << 20,  # noqa: E731
+                                   timeout_s=float(os.environ.get("BCG_AR_TIMEOUT_S", "30")), fault=f)
+    custom, status = establish(group, ctrl, make, torch.device("cuda", torch.cuda.current_device()), fault)
+    if custom is None:
+        return None, status
+    # routing limits measured on this group's links (RCCL groups; BCG_AR_CALIBRATE=0 keeps the
+    # built-in rule, =force also calibrates over gloo -- one-GPU tests of the mechanism)
+    cal = os.environ.get("BCG_AR_CALIBRATE", "1")
+    if cal == "force" or (cal != "0" and dist.get_backend(group) == "nccl"):
+        custom.calibrate(group, route=dist.get_backend(group) == "nccl", hidden=hidden)
+    return custom, status
 
 
 def data_parallel_group(tp: int):
@@ -149,8 +165,10 @@ def data_parallel_group(tp: int):
 
 def destroy():
     for ar in _CUSTOM_AR.values():
-        ar.close()
+        if ar is not None:
+            ar.close()
     _CUSTOM_AR.clear()
+    _CUSTOM_STATUS.clear()
     _TP_GROUPS.clear()
     _TP_CTRL.clear()
     _DP_GROUPS.clear()

@@ -17,18 +17,18 @@
 //     table used to pick for these shapes) has exactly these resources: 256 threads, 256
 //     AGPR accumulators, 16x16x32 MFMAs, LDS-DMA loads -- the schedule below is our own.
 //
-// Schedule (one K-tile t, stage s = t & 1 of a 2 x 64 KiB LDS ring; every index static):
+// Schedule (one K-tile t; LDS = a ring of five 32-KiB slots, tile t's X and W halves in slots
+// 2t and 2t+1 mod 5; every index static):
 //   phase A: 64 MFMAs of k-step 0 (fragments x0/w0 in registers)
-//            || 16 ds_read_b128 of k-step 1 of tile t (stage s) -> x1/w1
-//            then  s_waitcnt vmcnt(0) lgkmcnt(0); s_barrier
+//            || 16 ds_read_b128 of k-step 1 of tile t -> x1/w1
+//            || 8 LDS-DMA pieces of X(t+2) into the slot W(t-1) freed
+//            then  s_waitcnt vmcnt(8) lgkmcnt(0); s_barrier  (tile t+1 landed, X(t+2) may fly)
 //   phase B: 64 MFMAs of k-step 1 (x1/w1)
-//            || 16 LDS-DMA pieces of tile t+2 -> stage s
-//            || 16 ds_read_b128 of k-step 0 of tile t+1 (stage s^1) -> x0/w0
-// RAW: tile t+1's pieces were issued in phase B of tile t-1 and are waited for by every wave
-//      before the barrier that precedes their first read (phase B of tile t).
-// WAR: stage s was last read by tile t's k-step-0 reads (phase B of t-1) and k-step-1 reads
-//      (phase A of t); both drained (lgkmcnt(0)) by every wave before the barrier of tile t,
-//      after which tile t+2's pieces are issued.
+//            || 8 LDS-DMA pieces of W(t+2)
+//            || 16 ds_read_b128 of k-step 0 of tile t+1 -> x0/w0
+// RAW: a piece is waited for by every wave (counted vmcnt) before the barrier that precedes its
+//      first read.  WAR: a slot is refilled only after the barrier that follows its last reads
+//      (lgkmcnt(0) before that barrier).  Odd waves issue their pieces half a stride later.
 // One barrier per K-tile, a piece has 1.5 phases (~1500 cycles) to land.
 //
 // LDS: rows of 128 B (64 bf16 of K), the 16-B chunk c of row r at c ^ ((r >> 1) & 7): the
@@ -47,21 +47,11 @@
 #ifndef W4_GROUP_M
 #define W4_GROUP_M 8  // m-tiles per tile-order group (L2 reuse of both operands)
 #endif
-#ifndef W4_MFMA32
-#define W4_MFMA32 0  // 1: v_mfma_f32_32x32x16_bf16 (32 MFMAs per phase) instead of 16x16x32 (64)
-#endif
 // schedule knobs: first MFMA slot and slot stride of each memory-op stream (W4_SLOTS per phase)
-#if W4_MFMA32
-#define W4_SLOTS 32
-#else
 #define W4_SLOTS 64
-#endif
 // Defaults (measured, profiles/r4_gemm_w4/): the five-slot ring; phase A: the 16 k-step-1
 // reads in its first half, X(t+2)'s 8 pieces in its second; phase B: W(t+2)'s 8 pieces every
 // 8th slot, the 16 next-tile reads every 4th.
-#ifndef W4_RING5
-#define W4_RING5 1  // 1: five 32-KiB LDS slots, X(t+2) loaded in phase A(t), W(t+2) in phase B(t); 0: two stages
-#endif
 #ifndef W4_RA0
 #define W4_RA0 0  // phase A: k-step-1 reads
 #endif
@@ -78,7 +68,7 @@
 #define W4_DB0 0  // phase B: LDS-DMA pieces
 #endif
 #ifndef W4_DBS
-#define W4_DBS (W4_RING5 ? W4_SLOTS / 8 : W4_SLOTS / 16)
+#define W4_DBS (W4_SLOTS / 8)
 #endif
 #ifndef W4_RB0
 #define W4_RB0 (W4_SLOTS / 32)  // phase B: k-step-0 reads of the next tile
@@ -86,39 +76,17 @@
 #ifndef W4_RBS
 #define W4_RBS (W4_SLOTS / 16)
 #endif
-// timing ablations only (wrong results): pieces issued in phase B, and the first piece index
-#ifndef W4_ABL_NPIECE
-#define W4_ABL_NPIECE 16
-#endif
-#ifndef W4_ABL_PIECE0
-#define W4_ABL_PIECE0 0
-#endif
-#define W4_NPB (W4_RING5 ? 8 : W4_ABL_NPIECE)  // pieces issued in phase B
-#ifndef W4_STAGE_EPI
-#define W4_STAGE_EPI 0  // stores staged through the free ring slot, whole rows per store; measured: +-0.7 %, off
-#endif
-#ifndef W4_RES_PF
-#define W4_RES_PF 0  // residual tile -> L2 over an item's last N K-tiles (N % 4 == 0); measured: no gain
-#endif
-#ifndef W4_NT_STORE
-#define W4_NT_STORE 0  // non-temporal output stores; measured: 3-6 % slower
-#endif
+#define W4_NPB 8  // pieces issued in phase B (W(t+2)); phase A issues X(t+2)'s 8
 #ifndef W4_PERSIST
 #define W4_PERSIST 1  // one workgroup per CU streaming its tiles (split_k == 1; profiles/r4_gemm_w4)
 #endif
-#ifndef W4_STAGGER
-#define W4_STAGGER 1  // odd waves run the loop with their pieces half a stride later (+0.4-1 %, profiles/r4_gemm_w4)
-#endif
-#ifndef W4_M0_EARLY
-#define W4_M0_EARLY 0  // 1: each piece's M0 write one MFMA ahead of the piece (needs W4_DB0 >= 1)
-#endif
-static_assert(!W4_M0_EARLY || W4_DB0 >= 1, "M0 is written one slot before the first piece");
-static_assert(!W4_RING5 || (W4_DA0 + 7 * W4_DAS < W4_SLOTS && !W4_M0_EARLY), "RING5 schedule");
+static_assert(W4_DA0 + 7 * W4_DAS < W4_SLOTS, "phase A's X pieces fit the phase");
 
 namespace {
 
 constexpr int BM = 256, BN = 256, BK = 64;
-constexpr int A_BYTES = BM * 128, STAGE = A_BYTES + BN * 128;  // 64 KiB
+constexpr int W4_COUNTERS = 65536;  // the caller's arrival-counter array (one per tile)
+constexpr int A_BYTES = BM * 128;  // one operand's K-tile: 256 rows of 128 B
 enum Epilogue { EPI_STORE = 0, EPI_SILU_MUL = 1, EPI_RESIDUAL = 2 };
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -185,30 +153,25 @@ struct SchedF8Alt {
 __device__ uint64_t w4_stamps[1 << 17];
 #endif
 
-// M32: bf16 with v_mfma_f32_32x32x16_bf16; F8: e4m3 operands with v_mfma_scale_f32_32x32x64_f8f6f4
-// (unit E8M0 block scales; x_scale[m] * w_scale[n] applied in the epilogue)
-template <int EPI, bool M32, bool F8 = false>
+// F8: e4m3 operands with v_mfma_scale_f32_32x32x64_f8f6f4 (unit E8M0 block scales; x_scale[m] *
+// w_scale[n] applied in the epilogue)
+template <int EPI, bool F8 = false>
 __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_w4_kernel(
     const void* __restrict__ Xv, const void* __restrict__ Wv, const bf16_t* __restrict__ bias,
     const bf16_t* __restrict__ residual, bf16_t* __restrict__ C, float* __restrict__ ws,
     int* __restrict__ counters, int M, int N, int K, int ldc, int inter, int m_tiles, int n_tiles,
     int split_k, const float* __restrict__ x_scale, const float* __restrict__ w_scale) {
-  static_assert(!F8 || (EPI != EPI_SILU_MUL && !M32), "fp8: store / residual epilogues");
-  constexpr bool L32 = M32 || F8;                      // 32x32 accumulator layout
+  static_assert(!F8 || EPI != EPI_SILU_MUL, "fp8: store / residual epilogues");
+  constexpr bool L32 = F8;                             // 32x32 accumulator layout
   constexpr int SLOTS = F8 ? 16 : W4_SLOTS;            // MFMAs per phase
   constexpr int ESZ = F8 ? 1 : 2;                      // bytes per element
   const unsigned char* X = static_cast<const unsigned char*>(Xv);
   const unsigned char* W = static_cast<const unsigned char*>(Wv);
   // ONE shared array (cdna_hip_programming.md "Projection GEMM" item 4a)
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[W4_RING5 ? 5 * A_BYTES : 2 * STAGE];
-  // LDS byte offset of tile t's X (part 0) or W (part 1) half: two 64-KiB stages, or (RING5) a
-  // ring of five 32-KiB slots, tile t in slots 2t, 2t+1 (mod 5)
-  auto slot_off = [](int t, int part) -> uint32_t {
-    if constexpr (W4_RING5)
-      return static_cast<uint32_t>((2 * t + part) % 5) * A_BYTES;
-    else
-      return static_cast<uint32_t>(t & 1) * STAGE + part * A_BYTES;
-  };
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[5 * A_BYTES];
+  // LDS byte offset of tile t's X (part 0) or W (part 1) half: a ring of five 32-KiB slots, tile
+  // t in slots 2t, 2t+1 (mod 5)
+  auto slot_off = [](int t, int part) -> uint32_t { return static_cast<uint32_t>((2 * t + part) % 5) * A_BYTES; };
 
   // ---- work items.  split_k >= 1: nwg = tiles x k-splits.  A persistent launch (gridDim.x <
   // nwg, split_k == 1 only) gives workgroup b the items b, b + G, b + 2G, ...: one continuous
@@ -220,7 +183,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   // logical workgroup r (XCD-grouped: the workgroups of one XCD own one contiguous eighth of
   // the units) streams range r -- a partial first tile, whole tiles, a partial last tile.
   // Whole tiles take the ordinary in-stream epilogue; a partial segment stores its fp32 part
-  // (per wave, write-through) and the wave that arrives last for that (tile, wave) adds every
+  // (per wave, write-through) and the workgroup that arrives last for that tile adds every
   // segment's part after its stream and runs the epilogue -- nobody waits on another workgroup.
   // The tile quantisation of decode-size M goes away (gate_up at 704 rows: 408 tiles = 1.6 per
   // CU instead of two rounds).
@@ -311,20 +274,12 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   };
   // DMA cursor: stream tile t + 2 is K-tile dk0 + ktd of item jd, whose descriptors are dX / dW
   int jd = 0, ktd = 0, dk0 = gc.k0, dnk = gc.nk;
-  // stream tile t = K-tile kt of the DMA cursor's item; mode 0: M0 write + piece in one
-  // statement; 1: the piece only (M0 set earlier: set_m0)
-  auto dma = [&](int t, int kt, int q, const i32x4& sX, const i32x4& sW, int mode = 0) {
+  // stream tile t = K-tile kt of the DMA cursor's item: M0 write + piece in one statement
+  auto dma = [&](int t, int kt, int q, const i32x4& sX, const i32x4& sW) {
     const uint32_t kb = static_cast<uint32_t>(dk0 + kt) * (BK * 2);
     const bool isx = q < 8;
     const int i = q & 7;
     const uint32_t soff = __builtin_amdgcn_readfirstlane(kb);
-    if (mode == 1) {
-      if (isx)
-        asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(vX[i]), "s"(sX), "s"(soff) : "memory");
-      else
-        asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(vW[i]), "s"(sW), "s"(soff) : "memory");
-      return;
-    }
     const uint32_t m0v = dma_m0(t, q);
     if (isx) {
       asm volatile("s_mov_b32 m0, %3\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
@@ -337,9 +292,6 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
                    : "v"(vW[i]), "s"(sW), "s"(soff), "s"(m0v)
                    : "memory", "m0");
     }
-  };
-  auto set_m0 = [&](int t, int q) {
-    asm volatile("s_mov_b32 m0, %0" : : "s"(dma_m0(t, q)) : "memory", "m0");
   };
 
   // ---- fragments of one phase (32 of the K-tile's 64; half s = 0: chunks 0-3, 1: chunks 4-7):
@@ -355,9 +307,6 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     if constexpr (F8) {  // block (f >> 1) & 3, 16-B chunk f & 1 of the lane's 32 k (k = 32 (lane >> 5) + ...)
       const int blk = (f >> 1) & 3;
       off += (((4 * s + 2 * (lane >> 5) + (f & 1)) ^ rd_sw) << 4) + blk * 4096;
-    } else if constexpr (M32) {
-      const int ks = (f >> 2) & 1, blk = f & 3;
-      off += (((4 * s + 2 * ks + (lane >> 5)) ^ rd_sw) << 4) + blk * 4096;
     } else {
       off += (((4 * s + fq) ^ rd_sw) << 4) + (f & 7) * 2048;
     }
@@ -390,12 +339,6 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
                    : "+a"(acc[nb][mb])
                    : "v"(a), "v"(b), "v"(e8m0_one)
                    : "memory");
-    } else if constexpr (M32) {  // idx = ks * 16 + nb * 4 + mb
-      const int ks = idx >> 4, nb = (idx >> 2) & 3, mb = idx & 3;
-      asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0"
-                   : "+a"(acc[nb][mb])
-                   : "v"(wf[ks * 4 + nb]), "v"(xf[ks * 4 + mb])
-                   : "memory");
     } else {
       asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
                    : "+a"(acc[idx >> 3][idx & 7])
@@ -419,12 +362,6 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       }
     }
   };
-#ifdef W4_DESYNC  // timing experiment: odd workgroups start nk x W4_DESYNC cycles late (epilogues staggered)
-  if (blockIdx.x & 1) {
-    const uint64_t t0 = __builtin_amdgcn_s_memtime();
-    while (__builtin_amdgcn_s_memtime() - t0 < static_cast<uint64_t>(gc.nk) * W4_DESYNC) __builtin_amdgcn_s_sleep(10);
-  }
-#endif
   // ---- prologue: stream tiles 0 and 1 in flight, tile 0 landed, k-step 0 of tile 0 in registers ----
 #pragma unroll
   for (int q = 0; q < 16; ++q) dma(0, 0, q, dX, dW);
@@ -445,7 +382,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   //   32x32x16: block (nb, mb) lane: D[n = 32 nb + 8 g + 4 (lane >> 5) + e][m = 32 mb + (lane & 31)],
   //             registers 4 g + e;  i = 4 nb + g (g = 0..3)
   // value(nb, mb) returns the block's registers (accumulators, or the split-K slab sum).
-  auto epilogue = [&](const Geo& geo_c, auto value, uint32_t stage = 0xffffffffu) {
+  auto epilogue = [&](const Geo& geo_c, auto value) {
     constexpr int MB = L32 ? 32 : 16;
     constexpr int NG = L32 ? 4 : 1;  // quads per block
     // the lane index re-enters here through an opaque move: the epilogue's per-lane address
@@ -457,11 +394,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     const int m0 = geo_c.m0, n0 = geo_c.n0;
     auto row = [&](int j) { return m0 + wm * 128 + j * MB + ml; };
     auto st4 = [&](bf16_t* p, u16x4 v) {
-#if W4_NT_STORE  // streaming stores: the output tile does not displace the operand panels in L2
-      __builtin_nontemporal_store(v, reinterpret_cast<u16x4*>(p));
-#else
       *reinterpret_cast<u16x4*>(p) = v;
-#endif
     };
     if constexpr (!L32) {
       // 16x16 layout, buffer-addressed, 16-B accesses.  A store costs per cache line it touches
@@ -498,43 +431,13 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
           o[4 + e] = __uint_as_float(r[1]);
         }
       };
-      // With a staging slot (the ring slot tile t's W half left: free from the barrier after phase
-      // A(t) until phase A(t+1) refills it), the 8 columns go to LDS instead, 32 rows per pass,
-      // and come back row-major: every global store then writes 4 (SILU: 8) whole rows of the
-      // wave's 256 (128) B instead of 16 rows x 64 B.  XOR-swizzled 16-B chunks keep both the
-      // fragment-order writes and the row-order reads conflict-free.
-      constexpr int CH = SILU ? 8 : 16;  // 16-B chunks per staged row (the wave's columns)
-      const bool staged = stage != 0xffffffffu;
-      const uint32_t sbase = stage + static_cast<uint32_t>(wave) * (32 * CH * 16);
-      auto swz = [](int r) { return CH == 16 ? (r & 15) : ((r >> 1) & 7); };
       auto pack8 = [](const float (&o)[8]) {
         const u32x2 lo = __builtin_bit_cast(u32x2, pack4(o[0], o[1], o[2], o[3]));
         const u32x2 hi = __builtin_bit_cast(u32x2, pack4(o[4], o[5], o[6], o[7]));
         return u32x4{lo[0], lo[1], hi[0], hi[1]};
       };
       auto store8 = [&](int j, int p, const float (&o)[8]) {
-        if (staged) {  // row (j & 1) * 16 + fr of the pass, chunk 4 p + 2 (fq & 1) + (fq >> 1)
-          const int r = (j & 1) * 16 + fr, c = 4 * p + 2 * (fq & 1) + (fq >> 1);
-          *reinterpret_cast<u32x4*>(smem + sbase + (r * CH + (c ^ swz(r))) * 16) = pack8(o);
-          return;
-        }
         __builtin_amdgcn_raw_buffer_store_b128(pack8(o), rc, rowv + colv[p] + static_cast<uint32_t>(j * MB) * ldb, 0, 0);
-      };
-      // the pass of m-blocks j0, j0 + 1 (rows 16 j0 ..): read row-major, store whole rows
-      auto flush = [&](int j0) {
-        if (!staged) return;
-        constexpr int LPR = CH;           // lanes per row
-        constexpr int RPI = 64 / LPR;     // rows per instruction
-        const int c = lane & (LPR - 1);
-        const int cl = (SILU ? wn * 64 : wn * 128) + c * 8;
-        const uint32_t cv = SILU || n0 + cl < N ? static_cast<uint32_t>(cl) * 2 : 0x80000000u;
-#pragma unroll
-        for (int i = 0; i < 32 / RPI; ++i) {
-          const int r = i * RPI + lane / LPR;
-          const u32x4 v = *reinterpret_cast<const u32x4*>(smem + sbase + (r * CH + (c ^ swz(r))) * 16);
-          __builtin_amdgcn_raw_buffer_store_b128(v, rc, static_cast<uint32_t>(wm * 128 + j0 * MB + r) * ldb + cv, 0, 0);
-          if (i & 1) __builtin_amdgcn_sched_barrier(0);  // (two rows of reads in flight, not all)
-        }
       };
       if constexpr (SILU) {
 #pragma unroll
@@ -554,7 +457,6 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
             swap8(h[0], h[1], o);
             store8(j, p, o);
           }
-          if (j & 1) flush(j - 1);
           __builtin_amdgcn_sched_barrier(0);
         }
       } else {
@@ -611,7 +513,6 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
                 }
                 store8(j0 + jj, p, o);
               }
-            if (j0 & 1) flush(j0 - 1);  // one staging pass per two m-blocks
             __builtin_amdgcn_sched_barrier(0);
           }
         };
@@ -622,36 +523,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       }
       return;
     }
-    if constexpr (EPI == EPI_SILU_MUL) {
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const int m = row(j);
-        if (m >= M) continue;
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb) {
-          const auto blk = value(nb, j);
-          // 16-row blocks of the tile alternate gate / up of the same 16 features:
-          //   16x16x32: block pairs (nb, nb+1);  32x32x16: quads g and g + 2 of one block
-          if constexpr (M32) {
-#pragma unroll
-            for (int g = 0; g < 2; ++g) {
-              const int feat = (n0 >> 1) + wn * 64 + nb * 16 + 8 * g + 4 * (ln >> 5);
-              st4(C + static_cast<size_t>(m) * ldc + feat,
-                  pack4(silu(blk[4 * g]) * blk[4 * g + 8], silu(blk[4 * g + 1]) * blk[4 * g + 9],
-                        silu(blk[4 * g + 2]) * blk[4 * g + 10], silu(blk[4 * g + 3]) * blk[4 * g + 11]));
-            }
-          } else if (nb % 2 == 0) {
-            const auto u = value(nb + 1, j);
-            const int feat = (n0 >> 1) + wn * 64 + (nb >> 1) * 16 + 4 * fq;
-            st4(C + static_cast<size_t>(m) * ldc + feat,
-                pack4(silu(blk[0]) * u[0], silu(blk[1]) * u[1], silu(blk[2]) * u[2], silu(blk[3]) * u[3]));
-          }
-          // one block at a time: hoisting every accumulator read ahead of the stores would need
-          // the whole tile in VGPRs
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-    } else {
+    if constexpr (EPI != EPI_SILU_MUL) {  // (the 32x32 layout is fp8's: store / residual only)
       // batches of JG m-blocks; the residual quads of the next batch are loaded before this
       // batch is computed (one HBM round trip per batch, overlapped, instead of one per quad)
       constexpr int JG = L32 ? 1 : 2;
@@ -844,7 +716,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       for (int q = 0; q < 16; ++q) {
         const uint32_t soff = __builtin_amdgcn_readfirstlane(base + q * 1024);
         const uint32_t m0v = __builtin_amdgcn_readfirstlane(lds_w + b * 65536 + q * 1024);
-        asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen sc1 lds"
+        asm volatile("s_mov_b32 m0, %3\n\tbuffer_load_dwordx4 %0, %1, %2 offen sc1 lds"
                      :
                      : "v"(static_cast<uint32_t>(lane) * 16), "s"(srd), "s"(soff), "s"(m0v)
                      : "memory", "m0");
@@ -855,11 +727,13 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       for (int q = 0; q < 16; ++q) {
         const int f = 16 * g + q, i = f / (NB * QPB), j = (f / QPB) % NB, qq = f % QPB;
         const f32x4 v = *reinterpret_cast<const f32x4*>(smem + wave * 16384 + b * 65536 + q * 1024 + lane * 16);
+        // plain arithmetic: past the K-loop hipcc moves accumulators between AGPRs and VGPRs
+        // under pressure, and its AGPR write right before an asm read of that AGPR gets no
+        // wait states (asm reads here returned stale elements: one element of one block, in
+        // some launches)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float a;
-          // (s_nop 1: out here hipcc moves accumulators through AGPRs under pressure, and its
-          // AGPR write right before this read gets no wait states from it)
           asm volatile("s_nop 1\n\tv_accvgpr_read_b32 %0, %1" : "=v"(a) : "a"(acc[i][j][4 * qq + e]));
           a += v[e];
           asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(acc[i][j][4 * qq + e]) : "v"(a));
@@ -880,14 +754,12 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
           asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // this round landed, the next in flight
         else
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // the bytes of an LDS-DMA can land after its vmcnt has retired (measured: an element
-        // of a piece read stale, vmcnt(0) included): vmcnt, then a barrier, then the reads
-        // (cdna_hip_programming.md).  Every wave of the workgroup runs add_parts.
+        // (the bytes of an LDS-DMA can land after its vmcnt: a barrier before the reads, as in
+        // the reduce-scatter rounds -- every wave of the workgroup runs add_parts)
         asm volatile("s_barrier" ::: "memory");
         consume(g, g & 1);
       }
     }
-    asm volatile("s_nop 4" ::: "memory");  // (AGPR writes -> the epilogue's reads)
   };
   // stream-K: the logical workgroup whose range holds unit u; the tile's segments are those of
   // workgroups wg_of(T nk) .. wg_of((T + 1) nk - 1), segment (r, T) stored in part 2 r + (T is
@@ -934,24 +806,15 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 #pragma clang loop unroll(full)
     for (int idx = 0; idx < SLOTS; ++idx) {
       mf(idx, x1, w1);
-#ifndef W4_ABL_NODMA
-#if W4_M0_EARLY  // M0 written one MFMA before its piece (W4_DB0 >= 1)
-      if (idx + 1 >= Sch::DB0 && (idx + 1 - Sch::DB0) % Sch::DBS == 0 && (idx + 1 - Sch::DB0) / Sch::DBS < W4_NPB)
-        set_m0(t + 2, (idx + 1 - Sch::DB0) / Sch::DBS + W4_ABL_PIECE0 + (W4_RING5 ? 8 : 0));
-#endif
       if (idx >= Sch::DB0 && (idx - Sch::DB0) % Sch::DBS == 0 && (idx - Sch::DB0) / Sch::DBS < W4_NPB)
-        dma(t + 2, kt2, (idx - Sch::DB0) / Sch::DBS + W4_ABL_PIECE0 + (W4_RING5 ? 8 : 0), sX, sW, W4_M0_EARLY);
-#endif
-#ifndef W4_ABL_NOREAD
+        dma(t + 2, kt2, (idx - Sch::DB0) / Sch::DBS + 8, sX, sW);
       if (idx >= Sch::RB0 && (idx - Sch::RB0) % Sch::RBS == 0 && (idx - Sch::RB0) / Sch::RBS < 16)
         read_frag(t + 1, 0, (idx - Sch::RB0) / Sch::RBS, x0, w0);  // tile t+1 (garbage after the last)
-#endif
     }
   };
   auto run = [&](auto sch) {
     using Sch = decltype(sch);
     int ktc = 0, jc = 0;  // the live item's K-tile count and index
-    int pf_sink = 0;      // (W4_RES_PF)
 #ifdef W4_STAMPS  // diagnostic build: per-wave cycles in phase A / the wait + barrier / phase B / epilogues
     const uint64_t t_start = __builtin_amdgcn_s_memtime();
     uint64_t cyc_a = 0, cyc_w = 0, cyc_b = 0, cyc_e = 0, t_end = t_start;
@@ -967,52 +830,25 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 #pragma clang loop unroll(full)
       for (int idx = 0; idx < SLOTS; ++idx) {  // phase A
         mf(idx, x0, w0);
-#if W4_RING5  // X(t+2) into the slot W(t-1) left (free since the barrier of tile t-1)
         if (idx >= Sch::DA0 && (idx - Sch::DA0) % Sch::DAS == 0 && (idx - Sch::DA0) / Sch::DAS < 8)
           dma(t + 2, ktd, (idx - Sch::DA0) / Sch::DAS, sX, sX);
-#endif
-#ifdef W4_ABL_SPREAD  // timing ablation (racy): pieces 0..7 of tile t+2 issued in phase A
-        if (idx % (SLOTS / 8) == 2) dma(t + 2, ktd, idx / (SLOTS / 8), sX, sW);
-#endif
-#ifndef W4_ABL_NOREAD
         if (idx >= Sch::RA0 && (idx - Sch::RA0) % Sch::RAS == 0 && (idx - Sch::RA0) / Sch::RAS < 16)
           read_frag(t, 1, (idx - Sch::RA0) / Sch::RAS, x1, w1);
-#endif
       }
 #ifdef W4_STAMPS
       const uint64_t t_a = __builtin_amdgcn_s_memtime();
 #endif
-#if W4_RING5  // tile t+1 landed; X(t+2)'s 8 pieces of this phase may stay in flight
       asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#else
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
 #ifdef W4_STAMPS
       const uint64_t t_w = __builtin_amdgcn_s_memtime();
       cyc_a += t_a - t_end, cyc_w += t_w - t_a;
 #endif
-#if W4_RES_PF
-      if constexpr (EPI == EPI_RESIDUAL) {
-        // residual tile -> L2 over the item's last W4_RES_PF K-tiles (one dword per 128-B line,
-        // 4 lines per lane): the epilogue's reads then leave its HBM burst, which the stores
-        // of all 256 CUs saturate.  The sink VGPR stays live through the loop; its previous
-        // load is older than the 8 pieces the barrier's vmcnt(8) leaves, so it has landed.
-        asm volatile("" : : "v"(pf_sink));
-        const int r = ktc - (gc.nk - W4_RES_PF);
-        if (nsplit == 1 && r >= 0 && r % (W4_RES_PF / 4) == 0) {
-          const int line = (r / (W4_RES_PF / 4)) * 256 + tid;
-          const int row = min(gc.m0 + (line >> 2), M - 1), col = min(gc.n0 + (line & 3) * 64, N - 2);
-          const bf16_t* pf = residual + static_cast<size_t>(row) * ldc + col;
-          asm volatile("global_load_dword %0, %1, off" : "=v"(pf_sink) : "v"(pf) : "memory");
-        }
-      }
-#endif
       phase_b(t, ktd, sX, sW, sch);
-      // the MFMA D -> read wait states at the end of every K-tile, inside the loop: hipcc does
-      // not know an asm statement is an MFMA, so whatever it then does with the accumulators --
-      // the item-end block's reads, its register shuffles on the loop exit (a copy of a
-      // just-written block there read 16-lane rows not yet written) -- must come after these.
-      // (The wave waits for the MFMA pipe here instead of at the next phase's barrier.)
+      // the MFMA D -> read wait states at the end of every K-tile, inside the loop: whatever
+      // hipcc then does with the accumulators -- the item-end block's reads, its register
+      // shuffles on the loop exit (a copy of a just-written block there read 16-lane rows not
+      // yet written) -- comes after them.  (The wave waits here for the MFMA pipe it would wait
+      // for at the next phase's barrier anyway.)
       asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
 #ifdef W4_STAMPS
       t_end = __builtin_amdgcn_s_memtime();
@@ -1022,13 +858,9 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         // item done: its epilogue runs while the next item's first two K-tiles land (the MFMA
         // D -> read wait states are behind us: end of the K-tile above)
         if (gc.nk == nk_all)
-          epilogue(gc, [&](int i, int j) { return read_acc(acc[i][j]); }, W4_STAGE_EPI && W4_RING5 ? slot_off(t, 1) : 0xffffffffu);
+          epilogue(gc, [&](int i, int j) { return read_acc(acc[i][j]); });
         else
           sk_partial(gc);  // (stream-K: a tile cut by this workgroup's range)
-#if W4_STAGE_EPI && W4_RING5
-        // every wave's staging reads are done before phase A(t+1) loads X(t+3) into that slot
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
         // a counter wait hipcc sees: none of its epilogue loads is left pending across the back
         // edge (it would otherwise wait for them, i.e. drain everything, at the top of the next
         // K-tile).  The next item's pieces have had the whole epilogue to land.
@@ -1052,19 +884,15 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 #endif
   };
   if constexpr (F8) {
-    if (W4_STAGGER && (wave & 1))
+    if (wave & 1)
       run(SchedF8Alt{});
     else
       run(SchedF8{});
   } else {
-#if W4_STAGGER
     if (wave & 1)
       run(SchedAlt{});
     else
       run(SchedMain{});
-#else
-    run(SchedMain{});
-#endif
   }
   // every piece (the zero-range ones past the end included) has landed before the wave ends
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1077,15 +905,21 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         const Geo gp = geo(j);
         if (gp.nk == nk_all) return;  // a whole tile: its epilogue ran in the stream
         const int T = gp.tile;
-        // this wave's part of T is stored (sc1, drained); the wave that counts last for (T,
-        // wave) over the tile's segments sums them
-        int last = 0;
-        if (lane == 0) {
-          int* cnt = counters + T * 4 + wave;
-          last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nseg(T) - 1;
+        // every wave's part of T is stored (sc1, drained before the stream's end); the
+        // workgroup that counts last over the tile's segments sums them -- one decision per
+        // workgroup, so add_parts' barriers see all four waves
+        __syncthreads();
+        int* flag = reinterpret_cast<int*>(smem);
+        if (tid == 0) {
+          int* cnt = counters + T;
+          const int last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nseg(T) - 1;
           if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          flag[0] = last;
         }
-        if (!__builtin_amdgcn_readlane(last, 0)) return;
+        __syncthreads();
+        const int last = flag[0];
+        __syncthreads();  // every wave has read the flag before the part rounds overwrite it
+        if (!last) return;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         // zeros by VALU writes, not zero_acc's MFMAs: out here hipcc spills and reloads
         // accumulators between the asm statements, and its spill store of an asm MFMA's result
@@ -1102,7 +936,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         Geo g;
         g.tile = T;
         tile_geo(g);
-        epilogue(g, [&](int i, int jj) { return read_acc_tail(acc[i][jj]); });
+        epilogue(g, [&](int i, int jj) { return acc[i][jj]; });
       };
       if (n_items > 0) reduce_item(0);
       if (n_items > 1) reduce_item(n_items - 1);
@@ -1170,7 +1004,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   add_parts(slab, static_cast<uint32_t>(split_k) * BM * BN * 4, split_k - 1, [&](int k) {  // the other splits
     return static_cast<uint32_t>(k < gc.split ? k : k + 1) * (BM * BN * 4);
   });
-  epilogue(gc, [&](int i, int j) { return read_acc(acc[i][j]); });
+  epilogue(gc, [&](int i, int j) { return acc[i][j]; });
 }
 
 // compute units of the current device (one resident workgroup each: 160 KiB of LDS)
@@ -1197,7 +1031,7 @@ int launch_w4(const void* x, const void* w, const void* bias, const void* res, v
   // tiles x K-tiles units (split_k == 0, stream-K)
   const int grid = split_k == 0 ? w4_sk_grid(m_tiles * n_tiles, K / (F8 ? 128 : BK))
                    : W4_PERSIST && split_k == 1 ? std::min(nwg, w4_cus()) : nwg;
-  hipLaunchKernelGGL((gemm_w4_kernel<EPI, !F8 && W4_MFMA32 != 0, F8>), dim3(grid), dim3(256),
+  hipLaunchKernelGGL((gemm_w4_kernel<EPI, F8>), dim3(grid), dim3(256),
                      0, stream, x, w, static_cast<const bf16_t*>(bias), static_cast<const bf16_t*>(res),
                      static_cast<bf16_t*>(c), ws, cnt, M, N, K, ldc, inter, m_tiles, n_tiles, split_k, xs, wsc);
   return BCG_CHECK_LAUNCH();
@@ -1215,9 +1049,10 @@ BCG_API int bcg_gemm_w4_stamps(void* host, int n) {
 // Same contract as bcg_gemm_pp: epi 0 = store (+bias), 1 = silu(gate)*up into [M, inter],
 // 2 = residual + acc.  K % 64 == 0, K/64 >= split_k; N % 16 == 0 (a partial last n-tile is
 // masked); EPI 1: N == 2*inter, inter % 128 == 0.  split_k > 1: `ws` >= m_tiles*n_tiles*
-// split_k*65536 floats, `counters` >= m_tiles*n_tiles zeroed ints (left zeroed).
+// split_k*65536 floats, `counters` = 65536 ints, zeroed before first use (the last arriver of
+// each tile leaves its counter zeroed).
 // split_k == 0: stream-K (one workgroup per CU over the tiles x K-tiles units): `ws` >=
-// bcg_gemm_w4_sk_ws_floats() floats, `counters` >= 4*m_tiles*n_tiles zeroed ints (left zeroed).
+// bcg_gemm_w4_sk_ws_floats() floats, `counters` >= m_tiles*n_tiles zeroed ints (left zeroed).
 BCG_API int bcg_gemm_w4_sk_ws_floats() { return 2 * w4_cus() * BM * BN; }
 
 BCG_API int bcg_gemm_w4(int epi, const void* x, const void* w, const void* bias, const void* residual, void* c,
@@ -1228,10 +1063,11 @@ BCG_API int bcg_gemm_w4(int epi, const void* x, const void* w, const void* bias,
   // the output (and residual) offsets, a masked column's 0x80000000 bias included, stay 32-bit
   if (2ull * (M + BM) * (epi == EPI_SILU_MUL ? inter : N) >= (1ull << 31)) return -2;
   if (split_k != 1 && (!ws || !counters)) return -2;
-  if (split_k == 0) {  // stream-K: 4 counters per tile; the kernel's unit arithmetic is 32-bit
+  if (split_k == 0) {  // stream-K: a counter per tile; the kernel's unit arithmetic is 32-bit
     const long long tiles = 1ll * ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-    if (4 * tiles > (1 << 16) || tiles * (K / BK) * w4_cus() >= (1ll << 31)) return -2;
+    if (tiles > W4_COUNTERS || tiles * (K / BK) * w4_cus() >= (1ll << 31)) return -2;
   }
+  if (split_k > 1 && 1ll * ((M + BM - 1) / BM) * ((N + BN - 1) / BN) > W4_COUNTERS) return -2;
   float* wsf = static_cast<float*>(ws);
   int* cnt = static_cast<int*>(counters);
   switch (epi) {

@@ -30,8 +30,13 @@ static py::tuple py_compile_token_fsm(py::array_t<int32_t, py::array::c_style | 
   return py::make_tuple(next, dist);
 }
 
+#ifndef BCG_SOURCE_HASH
+#define BCG_SOURCE_HASH "unstamped"
+#endif
+
 PYBIND11_MODULE(_bcg_runtime, m) {
   m.doc() = "BCG MI355X engine native runtime (token FSM compiler, paged-KV block manager)";
+  m.attr("source_hash") = BCG_SOURCE_HASH;  // utils/build.py: hash of csrc/runtime/*
   m.def("compile_token_fsm", &py_compile_token_fsm, py::arg("trans"), py::arg("accept"),
         py::arg("tokens"), py::arg("vocab_rows"));
 

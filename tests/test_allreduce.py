@@ -303,3 +303,85 @@ def test_ipc_tp_collectives_real_shapes(tmp_path, world, back_to_back, cap_mb):
         if cap_mb >= 16:  # the 13 MB prefill message takes the two-shot form, decode the one-shot
             assert res["calls"].get("4", 0) == 4 and res["calls"].get("3", 0) == 2, (r, res)
         assert max(res["errs"]) < 2e-2, (r, res)
+
+
+class _GlooCustom:
+    """CPU stand-in of XGMIAllReduce for `establish`: the 'kernel' is the gloo all-reduce itself;
+    fault='ipc' fails this rank's construction the way the real one records it."""
+
+    def __init__(self, group, fault):
+        import torch.distributed as dist
+        self.group, self.cap_bytes, self.closed = group, 4 << 20, False
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        self.error = "ipc: injected hipIpcOpenMemHandle failure" if fault == "ipc" and rank == world - 1 else None
+
+    def all_reduce_(self, x, mode=None):
+        import torch.distributed as dist
+        dist.all_reduce(x, group=self.group)
+        return x
+
+    def close(self):
+        self.closed = True
+
+
+def _establish_worker(rank, world, port, out, fault):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    made = []
+
+    def make(f):
+        made.append(_GlooCustom(dist.group.WORLD, f))
+        return made[-1]
+    custom, status = CA.establish(dist.group.WORLD, dist.new_group(backend="gloo"), make, torch.device("cpu"), fault)
+    with open(f"{out}.{rank}", "w") as fh:
+        json.dump({"status": status, "custom": custom is not None, "closed": made[0].closed}, fh)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("fault", [None, "ipc", "mismatch"])
+def test_establish_agrees_on_fallback(tmp_path, world, fault):
+    """a failed IPC mapping or a custom result that differs from the process
+    group's all-reduce on ANY rank makes EVERY rank of the group fall back (same labelled status),
+    and the half-built custom all-reduce is closed; without faults the group keeps the kernels."""
+    out = str(tmp_path / "est")
+    mp.start_processes(_establish_worker, args=(world, _free_port(), out, fault), nprocs=world, join=True,
+                       start_method="spawn")
+    res = [json.load(open(f"{out}.{r}")) for r in range(world)]
+    assert len({r["status"] for r in res}) == 1, res
+    status = res[0]["status"]
+    if fault is None:
+        assert status == "on" and all(r["custom"] and not r["closed"] for r in res)
+    else:
+        assert status.startswith(f"fallback:rank{world - 1}:{fault}"), status
+        assert all(not r["custom"] and r["closed"] for r in res)
+
+
+def _establish_gpu_worker(rank, world, port, out, fault):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    make = lambda f: CA.XGMIAllReduce(dist.group.WORLD, cap_bytes=4 << 20, timeout_s=5.0, fault=f)  # noqa: E731
+    custom, status = CA.establish(dist.group.WORLD, dist.new_group(backend="gloo"), make,
+                                  torch.device("cuda", 0), fault)
+    if custom is not None:
+        dist.barrier()
+        custom.close()
+    with open(f"{out}.{rank}", "w") as fh:
+        json.dump({"status": status}, fh)
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fault", [None, "ipc", "mismatch"])
+def test_establish_real_kernels_one_gpu(tmp_path, fault):
+    """The same agreement with the real IPC-mapped kernels (2 processes on one GPU): the
+    cross-check passes bitwise without faults, and an injected failure falls back on both ranks."""
+    out = str(tmp_path / "estg")
+    mp.start_processes(_establish_gpu_worker, args=(2, _free_port(), out, fault), nprocs=2, join=True,
+                       start_method="spawn")
+    st = [json.load(open(f"{out}.{r}"))["status"] for r in range(2)]
+    assert st[0] == st[1], st
+    assert st[0] == "on" if fault is None else st[0].startswith(f"fallback:rank1:{fault}"), st

@@ -45,8 +45,10 @@ def test_bench_self_launches_two_ranks(tp, parallelism, replicas):
     assert out["config"]["global_batch"] == 2 * 5 * replicas
     d = out["detail"]
     assert d["decisions"] > 0 and out["value"] == pytest.approx(d["decisions"] / d["elapsed_s"], rel=1e-2)
-    # a step is one window: the timed region is K windows (+ the closing barrier)
-    assert 1000.0 <= out["ms_per_step"] < 1600.0
+    # a step is one window: the timed region is K windows (+ the closing barrier), and it fits in
+    # the process's own wall time (structural: no wall-clock upper bound on a shared box)
+    assert out["ms_per_step"] >= 1000.0
+    assert out["ms_per_step"] * out["steps"] <= 1000.0 * d["wall_since_start_s"]
     assert len(d["decisions_per_window_rank0"]) == 2
 
 
@@ -108,6 +110,11 @@ def test_bench_hostmodel_backend_reports_host_budget():
     out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
     h = out["detail"]["host"]
     assert out["detail"]["decisions"] > 0 and h["cpu_s_per_decision"] > 0
+    # the timed region's prompt sizes per phase and the context-limit counters
+    pt = out["detail"]["prompt_tokens_rank0"]
+    assert set(pt) == {"decide", "vote"} and all(0 < v["p50"] <= v["p95"] <= v["max"] for v in pt.values())
+    assert out["detail"]["context_rank0"]["rejects"] == 0
+    assert out["config"]["grammar"].endswith("ascii-text")
     assert h["min_replica_decisions_per_s"] > 0 and out["detail"]["tokens_per_s"] > 0
 
 

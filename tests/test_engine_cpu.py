@@ -244,3 +244,41 @@ def test_validity_aware_grammar_outputs_pass_simulator_rules(fresh_engine_state)
     for i, o in enumerate(outs):
         obj = json.loads(o.outputs[0].text)
         assert is_valid_vote(obj) if i % 3 == 2 else is_valid_decision(obj), obj
+
+
+def test_ascii_text_grammar_and_context_counters(fresh_engine_state):
+    """VERDICT r5 item 2.  The ASCII bench grammar: every free-text character the random model
+    writes is printable ASCII (no escapes / multi-byte UTF-8 that re-tokenise at several tokens per
+    character in later prompts).  A prompt at the context limit is answered "" and counted
+    (context_rejects); one whose context room is below the grammar's shortest output is counted
+    (context_short); prompt sizes are recorded per requested max_tokens."""
+    import json
+    from byzantine_consensus_llm_agents_amd.bcg import prompts as P
+    from byzantine_consensus_llm_agents_amd.bcg.simulation import is_valid_decision
+    from byzantine_consensus_llm_agents_amd.engine import GuidedDecodingParams, LLM, SamplingParams
+    llm = LLM("bcg/tiny-qwen3", backend="torch", seed=5, max_model_len=256, kv_cache_gb=0.05,
+              max_batch_seqs=16, budget_aware_json=True, validity_aware_json=10, ascii_text_json=True)
+    eng = llm.backend
+    sch = P.honest_decision_schema(0, 50)
+    ok = SamplingParams(temperature=1.0, max_tokens=120, guided_decoding=GuidedDecodingParams(json=sch))
+    outs = llm.generate([f"<|im_start|>user\nagent_{i}<|im_end|>\n<|im_start|>assistant\n" for i in range(6)],
+                        [ok] * 6)
+    for o in outs:
+        obj = json.loads(o.outputs[0].text)
+        assert is_valid_decision(obj), obj
+        for field in ("internal_strategy", "public_reasoning"):
+            assert all(0x20 <= ord(c) <= 0x7E for c in obj[field]), obj[field]
+    n_tok = lambda s: len(eng.tokenizer.encode(s))  # noqa: E731
+    filler = "word " * 400
+    long_p = filler[:len(filler)]
+    while n_tok(long_p) > 300:
+        long_p = long_p[:-50]
+    assert n_tok(long_p) >= 256
+    near = long_p
+    while n_tok(near) > 250:  # 6 tokens of room: below the decide grammar's shortest output
+        near = near[:-5]
+    outs = llm.generate([long_p, near], [ok, ok])
+    llm.shutdown()
+    assert outs[0].outputs[0].text == ""
+    assert eng.stats["context_rejects"] == 1 and eng.stats["context_short"] == 1
+    assert len(eng.prompt_lens[120]) == 8 and max(eng.prompt_lens[120]) == n_tok(long_p)

@@ -159,3 +159,22 @@ def test_validity_aware_grammar_matches_simulator_rules():
         assert not accepts(d, s)
     assert not accepts(db, '{"internal_strategy": "abcdefghij", "value": "abstain"}')  # reasoning now emitted
     assert accepts(db, '{"internal_strategy": "abcdefghij", "value": "abstain", "public_reasoning": "0123456789"}')
+
+
+def test_lone_surrogate_prompt_is_tokenised():
+    """A random model's JSON may hold a lone-surrogate escape (\\ud83d) that json.loads accepts; the
+    game quotes it in later prompts and the tokenizer refused the whole batch -- every prompt of
+    that game failed, the game ran to its round limit on defaults (VERDICT r5 weak 2's zombie
+    games).  encode_batch_safe replaces such characters with U+FFFD and counts the prompts."""
+    import json
+
+    from byzantine_consensus_llm_agents_amd.engine.tokenizer import encodable, load_tokenizer
+    tok = load_tokenizer("Qwen/Qwen3-14B")
+    bad = "reasoning " + json.loads('"abc\\ud83d xyz"')
+    with pytest.raises(TypeError):
+        tok.encode_batch([bad])
+    ids, n = tok.encode_batch_safe([bad, "plain text"])
+    assert n == 1 and ids[1] == tok.encode("plain text")
+    assert ids[0] == tok.encode(encodable(bad)) and "�" in encodable(bad)
+    ok = "plain text"
+    assert encodable(ok) is ok and tok.encode_batch_safe([ok]) == ([tok.encode(ok)], 0)
