@@ -85,9 +85,6 @@ def load_library(path: str = None) -> ctypes.CDLL:
         "bcg_gemm_nt_fp8": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
         "bcg_gemm_tile": [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)],
-        "bcg_w4r_shuffle": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
-        "bcg_gemm_w4r": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                         c_void_p],
         "bcg_gemm_num_cfgs": [],
         "bcg_guided_sample": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
@@ -357,46 +354,6 @@ def hip_ops() -> SimpleNamespace:
                                M, N, K, N // 2, split_k, _stream()), "gemm_nt")
         return out
 
-    def w4r_weight(w, silu=False):
-        """The pre-shuffled copy of w [N, K] that gemm_w4r reads (csrc/kernels/gemm_w4r.hip): per
-        64-row panel and 32-deep k-block the four MFMA A fragments, lane-major.  `silu`: w is
-        [gate; up] and the copy interleaves them by 16 rows (the fused SiLU epilogue's order).
-        Same shape and dtype as w, different element order; N % 64 == 0, K % 64 == 0."""
-        N, K = w.shape
-        _req(w.dtype == torch.bfloat16 and w.is_contiguous() and w.is_cuda, "w4r_weight: contiguous bf16 on the GPU")
-        _req(N % 64 == 0 and K % 64 == 0 and (not silu or (N // 2) % 16 == 0), f"w4r_weight: shape {N}x{K}")
-        out = torch.empty_like(w)
-        _check(lib.bcg_w4r_shuffle(_p(w), _p(out), N, K, N // 2 if silu else 0, _stream()), "w4r_shuffle")
-        return out
-
-    def w4r_supported(M, N, K, epi):
-        return (N % 64 == 0 and K % 64 == 0 and M > 0 and (epi != 1 or (N // 2) % 128 == 0)
-                and 2 * (M + 256) * K < 2 ** 31 and 2 * (M + 256) * (N // 2 if epi == 1 else N) < 2 ** 31)
-
-    def gemm_w4r(x, ws, epi=0, bias=None, residual=None, out=None):
-        """x [M, K] @ W^T with W given as its w4r_weight copy `ws` [N, K] (csrc/kernels/gemm_w4r.hip:
-        W register-fed, X through LDS); epilogue as gemm_nt (0 store(+bias), 1 silu(gate)*up ->
-        [M, N/2] from the silu copy, 2 residual + acc(+bias))."""
-        M, K = x.shape
-        N = ws.shape[0]
-        _req(x.dtype == torch.bfloat16 and ws.dtype == torch.bfloat16 and x.is_contiguous() and ws.is_contiguous()
-             and ws.shape[1] == K, "gemm_w4r: contiguous bf16 x [M,K], ws [N,K]")
-        _req(w4r_supported(M, N, K, epi), f"gemm_w4r: shape {M}x{N}x{K} epi {epi} unsupported")
-        width = N // 2 if epi == 1 else N
-        if out is None:
-            out = torch.empty(M, width, dtype=x.dtype, device=x.device)
-        _req(out.shape == (M, width) and out.is_contiguous() and out.dtype == torch.bfloat16, "gemm_w4r: out")
-        if bias is not None:
-            _req(epi != 1 and bias.shape == (N,) and bias.dtype == torch.bfloat16 and bias.is_contiguous(),
-                 "gemm_w4r: bias")
-        if epi == 2:
-            _req(residual is not None and residual.shape == (M, N) and residual.is_contiguous()
-                 and residual.dtype == torch.bfloat16, "gemm_w4r: residual [M,N] bf16")
-        _check(lib.bcg_gemm_w4r(epi, _p(x), _p(ws), _p(bias) if bias is not None else None,
-                                _p(residual) if residual is not None else None, _p(out), M, N, K, N // 2,
-                                _stream()), "gemm_w4r")
-        return out
-
     def linear_silu(x, w):
         """silu(x Wg^T) * (x Wu^T), W = [gate; up] -- K-ACT fused into the gate_up GEMM."""
         M, K = x.shape
@@ -570,7 +527,6 @@ def hip_ops() -> SimpleNamespace:
     return SimpleNamespace(name="hip", rmsnorm_fp8=rmsnorm_fp8, embed_rmsnorm_fp8=embed_rmsnorm_fp8,
                            linear_fp8_residual=linear_fp8_residual, linear=linear, linear_silu=linear_silu, linear_residual=linear_residual,
                            gemm_nt=gemm_nt, gemm_plan=plan, prepare_device=prepare_device,
-                           w4r_weight=w4r_weight, gemm_w4r=gemm_w4r, w4r_supported=w4r_supported,
                            register_stream=register_stream, quant_fp8=quant_fp8, add_rmsnorm_fp8=add_rmsnorm_fp8,
                            silu_mul_fp8=silu_mul_fp8, linear_fp8=linear_fp8, gemm_nt_fp8=gemm_nt_fp8, fp8_cfg=fp8_cfg, rmsnorm=rmsnorm, add_rmsnorm=add_rmsnorm, silu_mul=silu_mul,
                            embed_rmsnorm=embed_rmsnorm,
