@@ -657,6 +657,8 @@ def main(argv=None):
                        "parallelism": f"dp{world // args.tp}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
                        "hip_graphs": not args.no_graphs and getattr(llm.backend, "graphs_off_reason", None) is None,
                        "prefix_caching": not args.no_prefix_cache,
+                       "poll_every": C.ENGINE_CONFIG.get("poll_every"),
+                       "admit_max_wait": C.ENGINE_CONFIG.get("admit_max_wait"),
                        "grammar": "budget-aware" + ("" if args.plain_grammar else
                                                     f" + validity-aware({VALIDITY_MIN_VISIBLE})"
                                                     + ("" if args.unicode_text else " + ascii-text")),

@@ -103,6 +103,9 @@ ENGINE_CONFIG = {
     # only while >= admit_min_live rows decode.  3 vs 0, two A/B pairs on one GPU: 31.0k / 31.5k
     # vs 30.6k / 30.8k tokens/s (profiles/bench_r2_ab*_a*.json)
     "admit_max_wait": int(os.environ.get("BCG_ADMIT_MAX_WAIT", "3")),
+    # decode steps per burst (graph replays between two host polls of the completion state); a
+    # finished row idles until the poll after the burst that follows its last step
+    "poll_every": int(os.environ.get("BCG_POLL_EVERY", "8")),
     # run only full prefill chunks while the decode batch is fed: a wave's partial last chunk
     # waits (its prompts pending with their KV so far) up to this many more bursts for the
     # next wave (engine.py `_hold_tail`); 0 = run it at once

@@ -40,6 +40,10 @@ class AttnMeta:
     tiles: Optional[torch.Tensor] = None       # [n_tiles, 3] int32 prefill work list (HIP kernel)
     workspace: Optional[torch.Tensor] = None   # decode split-K scratch shared by all graphs (HIP)
     cascade: Optional[object] = None           # decode shared-prefix tables (engine/cascade.py)
+    # decode: the context lengths the attention reads (None = seq_lens).  The engine gives rows
+    # that already finished (they idle in the batch until the host reaps them) one token, so
+    # their KV is not streamed again every step; their outputs are ignored by the sampler
+    attn_seq_lens: Optional[torch.Tensor] = None
 
 
 class TPGroup:
@@ -326,7 +330,8 @@ class DecoderModel:
                                       L.get("q_norm"), L.get("k_norm"), c.rms_eps, self.cos_sin,
                                       k_cache, v_cache, li)
         if meta.decode:
-            return ops.paged_attention_decode(q, k_cache, v_cache, li, meta.block_tables, meta.seq_lens,
+            lens = meta.seq_lens if meta.attn_seq_lens is None else meta.attn_seq_lens
+            return ops.paged_attention_decode(q, k_cache, v_cache, li, meta.block_tables, lens,
                                               self.scale, meta.workspace, meta.cascade)
         return ops.paged_attention_prefill(q, k_cache, v_cache, li, meta.block_tables, meta.q_start,
                                            meta.seq_lens, self.scale, meta.max_q_len, meta.tiles)

@@ -282,3 +282,25 @@ def test_ascii_text_grammar_and_context_counters(fresh_engine_state):
     assert outs[0].outputs[0].text == ""
     assert eng.stats["context_rejects"] == 1 and eng.stats["context_short"] == 1
     assert len(eng.prompt_lens[120]) == 8 and max(eng.prompt_lens[120]) == n_tok(long_p)
+
+
+def test_finished_rows_skip_attention_same_outputs(fresh_engine_state, monkeypatch):
+    """Rows that finished idle in the decode batch until reaped; their attention reads one token
+    (engine.decode_meta attn_seq_lens) instead of the whole context.  Greedy outputs are identical
+    with and without the skip (the sampler ignores finished rows), rows finishing at different steps."""
+    from byzantine_consensus_llm_agents_amd.bcg import prompts as P
+    from byzantine_consensus_llm_agents_amd.engine import GuidedDecodingParams, LLM, SamplingParams
+    schemas = [P.honest_decision_schema(0, 50), P.vote_schema(P.HONEST_VOTE_OPTIONS)]
+    prompts = [f"<|im_start|>user\nagent_{i} round 3 " + "history " * (5 * i) + "<|im_end|>\n<|im_start|>assistant\n"
+               for i in range(6)]
+    params = [SamplingParams(temperature=0.0, max_tokens=[70, 12, 40, 9, 55, 20][i],
+                             guided_decoding=GuidedDecodingParams(json=schemas[i % 2])) for i in range(6)]
+    outs = {}
+    for skip in ("1", "0"):
+        monkeypatch.setenv("BCG_SKIP_DONE_ATTN", skip)
+        llm = LLM("bcg/tiny-qwen3", backend="torch", seed=9, max_model_len=512, kv_cache_gb=0.05,
+                  max_batch_seqs=8, budget_aware_json=True)
+        assert llm.backend._skip_done_attn == (skip == "1")
+        outs[skip] = [o.outputs[0].text for o in llm.generate(prompts, params)]
+        llm.shutdown()
+    assert outs["1"] == outs["0"]
