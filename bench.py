@@ -659,6 +659,7 @@ def main(argv=None):
                        "prefix_caching": not args.no_prefix_cache,
                        "poll_every": C.ENGINE_CONFIG.get("poll_every"),
                        "admit_max_wait": C.ENGINE_CONFIG.get("admit_max_wait"),
+                       "prefill_carry_bursts": C.ENGINE_CONFIG.get("prefill_carry_bursts"),
                        "grammar": "budget-aware" + ("" if args.plain_grammar else
                                                     f" + validity-aware({VALIDITY_MIN_VISIBLE})"
                                                     + ("" if args.unicode_text else " + ascii-text")),
