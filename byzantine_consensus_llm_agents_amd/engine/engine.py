@@ -367,6 +367,8 @@ class InferenceEngine:
             from .cascade import CascadeTables
             self.cascade = CascadeTables(cap, dev, self.args.kv_block_size)
         self._layout_dirty = True  # live rows changed since the cascade tables were built
+        rows_fn = getattr(self.ops, "prefill_tile_rows", None)
+        self._tile_rows = rows_fn(self.model.hd, self.kv_dtype() == torch.float8_e4m3fn) if rows_fn else 64
 
     def _phys(self, blocks: List[int]) -> List[int]:
         return [b + 1 for b in blocks]  # manager ids are shifted past scratch block 0
@@ -929,11 +931,12 @@ class InferenceEngine:
             if b == len(s.prompt_ids):
                 last_idx.append(q_start[-1] - 1)
                 last_rows.append(r)
-        # 64-query tiles for the HIP prefill kernel, deepest (most keys) first
+        # query tiles for the HIP prefill kernel (ops.prefill_tile_rows rows), deepest (most keys) first
+        tr = self._tile_rows
         tiles = []
         for i, (r, a, b) in enumerate(chunk):
-            for t in range(q_start[i], q_start[i + 1], 64):
-                tiles.append((b - (q_start[i + 1] - t), i, t, min(t + 64, q_start[i + 1])))
+            for t in range(q_start[i], q_start[i + 1], tr):
+                tiles.append((b - (q_start[i + 1] - t), i, t, min(t + tr, q_start[i + 1])))
         tiles.sort(key=lambda x: -x[0])
         i32 = torch.int32
         meta = AttnMeta(
@@ -944,6 +947,7 @@ class InferenceEngine:
             seq_lens=self._h2d(torch.tensor(seq_lens, dtype=i32)),
             q_start=self._h2d(torch.tensor(q_start, dtype=i32)),
             max_q_len=max(b - a for _, a, b in chunk),
+            tile_rows=tr,
             decode=False,
             logits_idx=self._h2d(torch.tensor(last_idx if last_idx else [0], dtype=torch.int64)))
         tokens = self._h2d(torch.tensor(toks, dtype=i32))

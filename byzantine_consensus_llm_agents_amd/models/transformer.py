@@ -38,6 +38,7 @@ class AttnMeta:
     decode: bool = False
     logits_idx: Optional[torch.Tensor] = None  # rows whose logits are needed
     tiles: Optional[torch.Tensor] = None       # [n_tiles, 3] int32 prefill work list (HIP kernel)
+    tile_rows: int = 64                        # rows per `tiles` entry (ops.prefill_tile_rows)
     workspace: Optional[torch.Tensor] = None   # decode split-K scratch shared by all graphs (HIP)
     cascade: Optional[object] = None           # decode shared-prefix tables (engine/cascade.py)
     # decode: the context lengths the attention reads (None = seq_lens).  The engine gives rows
@@ -334,7 +335,8 @@ class DecoderModel:
             return ops.paged_attention_decode(q, k_cache, v_cache, li, meta.block_tables, lens,
                                               self.scale, meta.workspace, meta.cascade)
         return ops.paged_attention_prefill(q, k_cache, v_cache, li, meta.block_tables, meta.q_start,
-                                           meta.seq_lens, self.scale, meta.max_q_len, meta.tiles)
+                                           meta.seq_lens, self.scale, meta.max_q_len, meta.tiles,
+                                           tile_rows=meta.tile_rows)
 
     def _forward_general(self, tokens, meta, k_cache, v_cache):
         """Tensor-parallel and / or fp8 forward, with the same fusions as the TP=1 bf16 path

@@ -19,7 +19,8 @@ def _torch_ops() -> SimpleNamespace:
         q_start = torch.arange(B + 1, dtype=torch.int32, device=q.device)
         return _ref.paged_attention(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale)
 
-    def prefill(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale, max_q_len=None, tiles=None):
+    def prefill(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale, max_q_len=None, tiles=None,
+                tile_rows=64):
         return _ref.paged_attention(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale)
 
     return SimpleNamespace(
@@ -31,6 +32,7 @@ def _torch_ops() -> SimpleNamespace:
         qk_norm_rope_kv_write=_ref.qk_norm_rope_kv_write,
         paged_attention_decode=decode,
         paged_attention_prefill=prefill,
+        prefill_tile_rows=lambda hd, kv_fp8=False: 64,
         silu_mul=_ref.silu_mul,
         linear_silu=_ref.linear_silu,
         linear_residual=_ref.linear_residual,

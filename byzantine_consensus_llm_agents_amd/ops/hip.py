@@ -16,6 +16,8 @@ import torch
 from ..utils.build import kernel_sources, kernels_source_hash, kernels_target
 
 _LIB = None
+# Rows per prefill attention tile unless BCG_PREFILL_TILE_ROWS says otherwise (prefill_tile_rows)
+PREFILL_TILE_ROWS = 128
 
 c_int, c_float, c_void_p, c_uint32, c_int64 = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int64
 
@@ -71,6 +73,9 @@ def load_library(path: str = None) -> ctypes.CDLL:
         "bcg_paged_attention_prefill": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                                         c_void_p, c_int, c_int, c_void_p],
+        "bcg_paged_attention_prefill32": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
+                                          c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
+                                          c_void_p, c_int, c_int, c_void_p],
         "bcg_decode_split_tokens": [c_int, c_int, c_int],
         "bcg_decode_max_splits": [c_int, c_int],
         "bcg_decode_max_context": [c_int],
@@ -230,7 +235,10 @@ def hip_ops() -> SimpleNamespace:
         return out
 
     def paged_attention_prefill(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale,
-                                max_q_len=None, tiles=None):
+                                max_q_len=None, tiles=None, tile_rows=64):
+        """tiles: [n_tiles, 3] int32 {sequence, first row, end row} of at most `tile_rows` rows.
+        64-row tiles run the 16x16 register kernel; 128 / 256-row tiles the LDS-staged 32x32
+        kernel (bf16 KV cache, head dim 128: `prefill_tile_rows` says which the engine builds)."""
         T, n_q, hd = q.shape
         L, NB, n_kv, BS, _ = k_cache.shape
         _req(tiles is not None and tiles.dtype == torch.int32 and tiles.dim() == 2 and tiles.shape[1] == 3,
@@ -238,11 +246,26 @@ def hip_ops() -> SimpleNamespace:
         _req(q.is_contiguous() and block_tables.dtype == torch.int32 and q_start.dtype == torch.int32
              and seq_lens.dtype == torch.int32, "prefill attention inputs")
         out = torch.empty(T, n_q * hd, dtype=q.dtype, device=q.device)
+        if tile_rows != 64:
+            _req(tile_rows in (128, 256) and hd == 128 and not _kv_fp8(k_cache, v_cache),
+                 "32x32 prefill attention: 128 / 256-row tiles, head dim 128, bf16 KV cache")
+            _check(lib.bcg_paged_attention_prefill32(
+                _p(q), _p(k_cache), _p(v_cache), layer, NB, n_kv, _p(block_tables), block_tables.shape[1],
+                _p(q_start), _p(seq_lens), _p(tiles), tiles.shape[0], n_q, hd, BS, scale, _p(out),
+                tile_rows, 0, _stream()), "paged_attention_prefill32")
+            return out
         _check(lib.bcg_paged_attention_prefill(
             _p(q), _p(k_cache), _p(v_cache), layer, NB, n_kv, _p(block_tables), block_tables.shape[1],
             _p(q_start), _p(seq_lens), _p(tiles), tiles.shape[0], n_q, hd, BS, scale, _p(out),
             4, _kv_fp8(k_cache, v_cache), _stream()), "paged_attention_prefill")
         return out
+
+    def prefill_tile_rows(hd, kv_fp8=False):
+        """Rows per prefill attention tile for this geometry (the tile table the caller builds):
+        128 / 256 select the LDS-staged 32x32 kernel (head dim 128, bf16 KV), 64 the 16x16 one.
+        BCG_PREFILL_TILE_ROWS overrides the default."""
+        rows = int(os.environ.get("BCG_PREFILL_TILE_ROWS", PREFILL_TILE_ROWS))
+        return rows if rows in (128, 256) and hd == 128 and not kv_fp8 else 64
 
     # Per-call GEMM dispatch log (VERDICT r3: which projection shapes reach a hand kernel, also
     # inside TP worker processes that no profiler sees): (M, N, K, epi, dtype) -> choice -> calls.
@@ -535,5 +558,6 @@ def hip_ops() -> SimpleNamespace:
                            decode_workspace_numel=decode_workspace_numel,
                            decode_max_context=lambda cascade=True: lib.bcg_decode_max_context(int(cascade)),
                            paged_attention_prefill=paged_attention_prefill,
+                           prefill_tile_rows=prefill_tile_rows,
                            sample_step=sample_step, dispatch_log=dispatch_log,
                            library=lib)

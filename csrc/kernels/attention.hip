@@ -1035,6 +1035,316 @@ void launch_prefill(int n_tiles, int n_q, const bf16_t* q, KVGeom g, const int* 
                      q_start, seq_lens, tiles, n_q, sl, out, n_tiles, xcd_order);
 }
 
+// ------------------------------------------------- prefill, 32x32 MFMA, LDS-staged K/V
+// The 16x16 kernel above holds 510 registers (one wave per SIMD), so nothing hides a wave's
+// softmax VALU or its reload latency behind another wave's MFMAs.  This form is built for two
+// waves per SIMD (<= 256 registers): a workgroup = NW waves x 32 query rows of ONE query head
+// (tiles of 32 * NW rows), K/V of 64-token chunks staged ONCE per workgroup in an NS-slot LDS
+// ring by LDS-DMA (32 x 1-KiB pieces per chunk, P = 32 / NW per wave), one s_barrier per chunk.
+//
+// Swapped products on v_mfma_f32_32x32x16_bf16 (A[m = l&31][k = 8(l>>5)+j], B[k][n = l&31],
+// C[m = 8(i>>2) + 4(l>>5) + (i&3)][n = l&31]):
+//   S^T = K Q^T     A = K rows from LDS, B = Q fragments in registers (8 x bf16x8);
+//   O^T += V^T P^T  A = V^T rows from LDS (the V cache is [hd][16 tokens] per block),
+//                   B = P^T straight from the S^T accumulators of the same lane.
+// Token permutation (per 32-token tile u): S^T row m = 16s + 8a + 4h + b holds token
+// 32u + 16s + 8h + 4a + b, so accumulator i of lane half h is token 32u + 16(i>>3) + 8h + (i&7):
+// P.V k-step 2u + (i>>3) takes the lane's own 8 consecutive accumulators as its B operand, and
+// the matching V^T operand is ONE 16-byte read (8 consecutive tokens of a V^T row).  No
+// cross-lane traffic except one permlane32_swap per chunk for the column max.
+// LDS images (no bank conflicts for the 16-lane groups of ds_read_b128):
+//   K: row t (token of the chunk) at t * 256, its 16-B chunk p stored at slot p ^ (t & 15);
+//   V: block s at 16 KiB + s * 4 KiB, row d at d * 32, 16-B half e stored at e ^ ((d >> 3) & 1).
+// The source side of each LDS-DMA lane applies the swizzle (LDS destinations are consecutive).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+#ifndef PREFILL32_KFIRST
+#define PREFILL32_KFIRST 1
+#endif
+#ifndef PREFILL32_SCHED
+#define PREFILL32_SCHED 0  // pin the LDS reads one step ahead of their MFMAs (sched_group_barrier)
+#endif
+constexpr int PREFILL32_MAX_BLOCKS = 1024;  // block-table width the 32x32 kernel stages in LDS (16k tokens)
+
+// One 64-token chunk of prefill_attn32_kernel for one wave (32 query columns):
+//   attn32_scores  S^T = K Q^T, the column max m_new (the online softmax rescales EVERY chunk:
+//                  a data-dependent rescale branch made hipcc copy the 64 O accumulators between
+//                  register sets on every chunk -- 64 v_mov_b64 against 32 v_pk_mul here),
+//                  O and the partial sums scaled by 2^(m - m_new), t = S * scale - m_new;
+//   attn32_pv      P = 2^t, partial row sums, O^T += V^T P^T.
+// MASKED: rel_pos = (token of accumulator 0) - (this column's position) (causal mask),
+// rel_ctx = (token of accumulator 0) - ctx (V of tokens past the context is zeroed).
+// A column's first chunk always holds a visible key (token 0), so m is finite after it.
+template <bool MASKED>
+__device__ __forceinline__ void attn32_scores(const unsigned char* slot, int k_lane, const bf16x8 (&bq)[8],
+                                              float scale_log2, int rel_pos, float& m, float& lsum,
+                                              f32x16 (&o)[4], float (&t)[32]) {
+  f32x16 s0 = f32x16{}, s1 = f32x16{};
+#if PREFILL32_KFIRST  // every K operand of the chunk read before the first MFMA (64 VGPRs, counted waits)
+  bf16x8 ka[8][2];
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    const unsigned char* p = slot + (k_lane ^ (kk << 5));
+    ka[kk][0] = *reinterpret_cast<const bf16x8*>(p);
+    ka[kk][1] = *reinterpret_cast<const bf16x8*>(p + 32 * 256);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler sinks them to their uses)
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[kk][0], bq[kk], s0, 0, 0, 0);
+    s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[kk][1], bq[kk], s1, 0, 0, 0);
+  }
+#else
+  bf16x8 a0 = *reinterpret_cast<const bf16x8*>(slot + k_lane);
+  bf16x8 a1 = *reinterpret_cast<const bf16x8*>(slot + k_lane + 32 * 256);
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {  // the next k-step's K operands are read before this one's MFMAs
+    bf16x8 n0 = a0, n1 = a1;
+    if (kk + 1 < 8) {
+      const unsigned char* ka = slot + (k_lane ^ ((kk + 1) << 5));
+      n0 = *reinterpret_cast<const bf16x8*>(ka);
+      n1 = *reinterpret_cast<const bf16x8*>(ka + 32 * 256);
+    }
+    s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq[kk], s0, 0, 0, 0);
+    s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bq[kk], s1, 0, 0, 0);
+    a0 = n0;
+    a1 = n1;
+  }
+#endif
+  // accumulator i of tile u is token 32u + 16(i>>3) + 8h + (i&7)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    t[i] = s0[i];
+    t[16 + i] = s1[i];
+  }
+  if constexpr (MASKED) {
+#pragma unroll
+    for (int i = 0; i < 32; ++i)
+      if (rel_pos + 32 * (i >> 4) + 16 * ((i >> 3) & 1) + (i & 7) > 0) t[i] = -INFINITY;
+  }
+  float v = t[0];
+#pragma unroll
+  for (int i = 1; i < 31; i += 2) v = vmax3(v, t[i], t[i + 1]);
+  v = vmax(v, t[31]);
+  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = vmax(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * scale_log2;  // column max (log2 units)
+  const float m_new = vmax(m, v);   // finite from the column's first chunk on
+  const float alpha = fast_exp2(m - m_new);  // m = -inf: 0
+  m = m_new;
+  lsum *= alpha;
+  const f32x2 al = {alpha, alpha};
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+      const f32x2 x = f32x2{o[dt][i], o[dt][i + 1]} * al;
+      o[dt][i] = x.x;
+      o[dt][i + 1] = x.y;
+    }
+  const f32x2 sc = {scale_log2, scale_log2}, mm = {m_new, m_new};
+#pragma unroll
+  for (int i = 0; i < 32; i += 2) {  // two scores per v_pk_fma_f32 (masked: -inf stays -inf)
+    const f32x2 x = f32x2{t[i], t[i + 1]} * sc - mm;
+    t[i] = x.x;
+    t[i + 1] = x.y;
+  }
+}
+
+template <bool MASKED>
+__device__ __forceinline__ void attn32_pv(const unsigned char* slot, int v_lane, int rel_ctx, const float (&t)[32],
+                                          float& lsum, f32x16 (&o)[4]) {
+  // P = 2^t, lane-local partial row sums (packed adds); P^T operands of the four 16-token k-steps
+  bf16x8 bp[4];
+  f32x2 ps = {0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 32; i += 2) {
+    const f32x2 p = {fast_exp2(t[i]), fast_exp2(t[i + 1])};
+    ps += p;
+    bp[i >> 3][i & 7] = static_cast<__bf16>(p.x);
+    bp[i >> 3][(i & 7) + 1] = static_cast<__bf16>(p.y);
+  }
+  lsum += ps.x + ps.y;
+  // O^T += V^T P^T (k-step s = block s of the chunk, this lane half's 8 tokens); each V operand
+  // is read one MFMA ahead
+  const unsigned char* vb = slot + v_lane;
+  u32x4 va = *reinterpret_cast<const u32x4*>(vb);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    uint32_t keep[4] = {~0u, ~0u, ~0u, ~0u};
+    if constexpr (MASKED) {  // stale bytes past the context may be non-finite: zero them
+#pragma unroll
+      for (int j2 = 0; j2 < 4; ++j2) {
+        const int tk = rel_ctx + 16 * s + 2 * j2;  // token - ctx
+        keep[j2] = (tk < 0 ? 0x0000ffffu : 0u) | (tk + 1 < 0 ? 0xffff0000u : 0u);
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int nx = 4 * s + dt + 1;
+      u32x4 vn = va;
+      if (nx < 16) vn = *reinterpret_cast<const u32x4*>(vb + (nx >> 2) * 4096 + (nx & 3) * 1024);
+      if constexpr (MASKED) {
+#pragma unroll
+        for (int j2 = 0; j2 < 4; ++j2) va[j2] &= keep[j2];
+      }
+      o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, va), bp[s], o[dt], 0, 0, 0);
+      va = vn;
+#if PREFILL32_SCHED
+      if (nx < 16) __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+#endif
+    }
+  }
+}
+
+template <int NW, int NS>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void prefill_attn32_kernel(
+    const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
+    const int* __restrict__ q_start, const int* __restrict__ seq_lens, const int* __restrict__ tiles, int n_q,
+    float scale_log2, bf16_t* __restrict__ out) {
+  constexpr int HD = 128, KC = 64;                   // head dim, tokens per chunk
+  constexpr int KBYTES = KC * HD * 2, SLOT = 2 * KBYTES;  // K (then V) image of one chunk: 16 KiB each
+  constexpr int P = 32 / NW;                         // 1-KiB DMA pieces per wave per chunk
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(NS >= 2 && NS <= 4, "ring depth");
+  __shared__ __attribute__((aligned(1024))) unsigned char ring[NS * SLOT];
+
+  const int tile = blockIdx.x, qh = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = lane & 31, h = lane >> 5;
+  const int b = tiles[3 * tile], q_begin = tiles[3 * tile + 1], q_end = tiles[3 * tile + 2];
+  const int ctx = seq_lens[b];
+  const int pos0 = ctx - (q_start[b + 1] - q_start[b]) - q_start[b];  // position of packed row r = pos0 + r
+  const int kvh = qh / (n_q / g.n_kv);
+  const int* table = block_tables + static_cast<size_t>(b) * max_blocks;
+  const int nblk = (ctx + BS - 1) / BS;
+  const int wg_last = min(q_begin + 32 * NW, q_end) - 1;
+  const int nchunk = (pos0 + wg_last + KC) / KC;      // chunks the workgroup stages (uniform)
+  const int row0 = q_begin + 32 * w;
+  const bool active = row0 < q_end;                   // wave-uniform
+  const int w_last = min(row0 + 31, q_end - 1);
+  const int w_chunks = active ? (pos0 + w_last + KC) / KC : 0;          // chunks this wave computes
+  const int n_full = active ? min((pos0 + row0 + 1) / KC, w_chunks) : 0;  // ... seen in full by all its rows
+  // this lane's query column; columns past q_end compute as the tile's last row (never stored)
+  const int my_row = min(row0 + col, q_end - 1);
+  const int pos_q = pos0 + my_row;
+
+  // ---- LDS-DMA issue of chunk c into slot c % NS (this wave's P pieces) ----
+  // The sequence's block ids are staged in LDS once: a scalar load of a table entry per piece
+  // (each followed by its lgkmcnt wait) serialised ~8 round trips into every chunk.
+  __shared__ int blk_ids[PREFILL32_MAX_BLOCKS];
+  for (int i = threadIdx.x; i < 4 * nchunk; i += 64 * NW) blk_ids[i] = table[min(i, nblk - 1)];
+  const unsigned char* kc = reinterpret_cast<const unsigned char*>(g.k);
+  const unsigned char* vc = reinterpret_cast<const unsigned char*>(g.v);
+  const size_t head_base = static_cast<size_t>(g.layer) * g.num_blocks;
+  // lane parts of the source offsets (K piece rows 4 (i & 3) + lane / 16 of a block, its 16-B
+  // chunk (lane & 15) ^ row; V^T piece rows d = 32 (i & 3) + lane / 2, half (lane & 1) ^ bit 3 of d)
+  const int lane_kx = (lane & 15) ^ (lane >> 4), lane_k = (lane >> 4) * 256;
+  const int lane_v = (lane >> 1) * 32 + (((lane ^ (lane >> 4)) & 1) << 4);
+  auto issue = [&](int c) __attribute__((always_inline)) {
+    unsigned char* slot = ring + (c % NS) * SLOT;
+    int blk[P];
+#pragma unroll
+    for (int pi = 0; pi < P; ++pi) blk[pi] = blk_ids[4 * c + (((w * P + pi) & 15) >> 2)];
+#pragma unroll
+    for (int pi = 0; pi < P; ++pi) {
+      const int i = w * P + pi;  // piece 0..31, wave-uniform
+      const int r4 = i & 3;
+      const size_t base = ((head_base + __builtin_amdgcn_readfirstlane(blk[pi])) * g.n_kv + kvh) * (BS * HD * 2);
+      if (i < 16)  // K rows 4i .. 4i+3 of the chunk
+        __builtin_amdgcn_global_load_lds(kc + base + (r4 * 1024 + lane_k + ((lane_kx ^ (4 * r4)) << 4)),
+                                         slot + i * 1024, 16, 0, 0);
+      else  // V^T rows 32 (i & 3) .. + 31 of block (i & 15) / 4
+        __builtin_amdgcn_global_load_lds(vc + base + (r4 * 1024 + lane_v), slot + KBYTES + (i - 16) * 1024, 16,
+                                         0, 0);
+    }
+  };
+
+  // Q^T operands: lane (col, h) holds dims 16 kk + 8 h .. + 7 of its row
+  bf16x8 bq[HD / 16];
+  {
+    const bf16_t* qrow = q + (static_cast<size_t>(my_row) * n_q + qh) * HD + 8 * h;
+    u32x4 raw[HD / 16];
+#pragma unroll
+    for (int kk = 0; kk < HD / 16; ++kk) raw[kk] = *reinterpret_cast<const u32x4*>(qrow + 16 * kk);
+    // resolve the Q loads before the first DMA: inside the loop the compiler's wait for them
+    // would be a vmcnt(0) that drains the ring
+#pragma unroll
+    for (int kk = 0; kk < HD / 16; ++kk) {
+      asm volatile("" : "+v"(raw[kk]));
+      bq[kk] = __builtin_bit_cast(bf16x8, raw[kk]);
+    }
+  }
+  __syncthreads();  // block ids staged
+#pragma unroll
+  for (int c = 0; c < NS - 1; ++c)
+    if (c < nchunk) issue(c);
+
+  // K operand addresses: S^T row m = col holds token t0(m) (tile u = 0; u = 1 is t0 + 32, the same
+  // swizzle); 16-B chunk 2 kk + h of that row sits at slot (2 kk + h) ^ (t0 & 15), i.e. at byte
+  // offset k_lane ^ (kk << 5) (2 kk and h are disjoint bits)
+  const int t0 = 16 * (col >> 4) + 8 * ((col >> 2) & 1) + 4 * ((col >> 3) & 1) + (col & 3);
+  const int k_lane = t0 * 256 + (((t0 & 15) ^ h) << 4);
+  const int v_lane = KBYTES + col * 32 + (((h ^ (col >> 3)) & 1) << 4);
+
+  f32x16 o[HD / 32];
+#pragma unroll
+  for (int dt = 0; dt < HD / 32; ++dt) o[dt] = f32x16{};
+  float m = -INFINITY, lsum = 0.f;  // running max (log2 units, column-uniform), this lane's partial sum
+
+  // chunk c's pieces landed and its successor's slot is free: wait + barrier, then the DMA of
+  // chunk c + NS - 1 (every wave runs this for every chunk of the workgroup)
+  auto sync = [&](int c) __attribute__((always_inline)) {
+    const int ahead = min(NS - 2, nchunk - 1 - c);  // later chunks whose pieces may still fly
+#ifndef PREFILL32_ABL_NOWAIT  // timing ablation only (wrong results): the DMA is never waited for
+    if (ahead >= 2) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * P) : "memory");
+    } else if (ahead == 1) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+#else
+    (void)ahead;
+#endif
+    __builtin_amdgcn_s_barrier();  // ... and every wave is past chunk c - 1: its slot is free
+    asm volatile("" ::: "memory");
+    if (c + NS - 1 < nchunk) issue(c + NS - 1);
+  };
+  auto slot_of = [&](int c) { return static_cast<const unsigned char*>(ring + (c % NS) * SLOT); };
+  int c = 0;
+  float t[32];
+  // chunks every row of the wave sees in full, then the diagonal (and context-end) chunks --
+  // causal mask, V past the context zeroed -- in loops of their own (no branch on O inside)
+  for (; c < n_full; ++c) {
+    sync(c);
+    attn32_scores<false>(slot_of(c), k_lane, bq, scale_log2, 0, m, lsum, o, t);
+    attn32_pv<false>(slot_of(c), v_lane, 0, t, lsum, o);
+  }
+  for (; c < w_chunks; ++c) {
+    sync(c);
+    attn32_scores<true>(slot_of(c), k_lane, bq, scale_log2, c * KC + 8 * h - pos_q, m, lsum, o, t);
+    attn32_pv<true>(slot_of(c), v_lane, c * KC + 8 * h - ctx, t, lsum, o);
+  }
+  for (; c < nchunk; ++c) sync(c);  // chunks in the causal future of every row of this wave
+  if (!active || row0 + col >= q_end) return;
+  {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum), __float_as_uint(lsum), false, false);
+    lsum = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+  }
+  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+  bf16_t* orow = out + (static_cast<size_t>(row0 + col) * n_q + qh) * HD + 4 * h;
+#pragma unroll
+  for (int dt = 0; dt < HD / 32; ++dt)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {  // O^T rows d = 32 dt + 8 gq + 4 h + (0..3) of this lane's column
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      bf16x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = static_cast<__bf16>(o[dt][4 * gq + i] * inv);  // v_cvt_pk_bf16_f32 (RNE)
+      *reinterpret_cast<bf16x4*>(orow + 32 * dt + 8 * gq) = v;
+    }
+}
+
 }  // namespace
 
 // Split size for a decode batch.  Measured on MI355X (tools/bench_ops.py, Qwen3-14B
@@ -1123,6 +1433,39 @@ BCG_API int bcg_paged_attention_prefill(const void* q, const void* k_cache, cons
                                       ob, stream)
            : launch_prefill<64, false>(n_tiles, n_q, qb, g, block_tables, max_blocks, q_start, seq_lens, tiles, sl,
                                        ob, stream);
+  else
+    return -2;
+  return BCG_CHECK_LAUNCH();
+}
+
+// The 32x32 LDS-staged form (prefill_attn32_kernel): `tiles` holds tiles of at most tile_rows
+// rows -- 128 (4 waves, 2-slot ring, two workgroups per CU) or 256 (8 waves, 3-slot ring).
+// bf16 KV cache and head dim 128 only (-2 otherwise: the caller uses the 16x16 kernel).
+#ifndef PREFILL32_NS4
+#define PREFILL32_NS4 2
+#endif
+#ifndef PREFILL32_NS8
+#define PREFILL32_NS8 3
+#endif
+BCG_API int bcg_paged_attention_prefill32(const void* q, const void* k_cache, const void* v_cache, int layer,
+                                          int num_blocks, int n_kv, const int* block_tables, int max_blocks,
+                                          const int* q_start, const int* seq_lens, const int* tiles, int n_tiles,
+                                          int n_q, int hd, int block_size, float scale, void* out, int tile_rows,
+                                          int kv_fp8, hipStream_t stream) {
+  if (block_size != BS || n_kv <= 0 || n_q % n_kv || n_tiles <= 0 || n_q > 65535 || hd != 128 || kv_fp8 ||
+      max_blocks > PREFILL32_MAX_BLOCKS)
+    return -2;
+  KVGeom g{static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), layer, num_blocks, n_kv};
+  const float sl = scale * LOG2E;
+  const bf16_t* qb = static_cast<const bf16_t*>(q);
+  bf16_t* ob = static_cast<bf16_t*>(out);
+  const dim3 grid(n_tiles, n_q);
+  if (tile_rows == 128)
+    hipLaunchKernelGGL((prefill_attn32_kernel<4, PREFILL32_NS4>), grid, dim3(256), 0, stream, qb, g, block_tables,
+                       max_blocks, q_start, seq_lens, tiles, n_q, sl, ob);
+  else if (tile_rows == 256)
+    hipLaunchKernelGGL((prefill_attn32_kernel<8, PREFILL32_NS8>), grid, dim3(512), 0, stream, qb, g, block_tables,
+                       max_blocks, q_start, seq_lens, tiles, n_q, sl, ob);
   else
     return -2;
   return BCG_CHECK_LAUNCH();

@@ -196,6 +196,44 @@ def test_paged_attention_prefill(hip, n_q, n_kv, hd, kv_dtype):
     _close(out, ref, atol=2e-2)
 
 
+@pytest.mark.parametrize("tile_rows", [128, 256])
+@pytest.mark.parametrize("n_q,n_kv", [(40, 8), (64, 8), (8, 8)])
+def test_paged_attention_prefill32(hip, n_q, n_kv, tile_rows):
+    """LDS-staged 32x32 prefill kernel against the fp32 reference: partial tiles, cached prefixes
+    (full and partial 64-token chunks), a 1400-token context, several layers, and NaN in the
+    cache slots past every context (the kernel must never let them reach the output)."""
+    gen = torch.Generator().manual_seed(5)
+    hd, L, layer = 128, 2, 1
+    spec = [(0, 1), (0, 37), (16, 50), (32, 64), (0, 300), (160, 129), (400, 1000), (0, 257), (700, 33)]
+    ctx = [a + b for a, b in spec]
+    B, NB = len(spec), 512
+    k, v = _caches(L, NB, n_kv, hd)
+    tables = _tables(B, ctx, NB, 128, gen)
+    for b, n in enumerate(ctx):  # poison the tail of each sequence's last block
+        if n % 16:
+            blk = int(tables[b, (n - 1) // 16])
+            k[layer, blk, :, n % 16:, :] = float("nan")
+            v[layer, blk, :, :, n % 16:] = float("nan")
+    q_start = [0]
+    for _, n in spec:
+        q_start.append(q_start[-1] + n)
+    q = torch.randn(q_start[-1], n_q, hd, device="cuda", dtype=torch.bfloat16)
+    qs = torch.tensor(q_start, dtype=torch.int32, device="cuda")
+    seq = torch.tensor(ctx, dtype=torch.int32, device="cuda")
+    ref = R.paged_attention(q, k, v, layer, tables, qs, seq, hd ** -0.5)
+    tiles = []
+    for i in range(B):
+        for t in range(q_start[i], q_start[i + 1], tile_rows):
+            tiles.append((i, t, min(t + tile_rows, q_start[i + 1])))
+    tiles = torch.tensor(tiles[::-1], dtype=torch.int32, device="cuda")
+    assert hip.prefill_tile_rows(hd) in (64, 128, 256) and hip.prefill_tile_rows(64) == 64
+    for _ in range(2):  # repeated launches: the LDS ring starts clean every time
+        out = hip.paged_attention_prefill(q, k, v, layer, tables, qs, seq, hd ** -0.5, None, tiles,
+                                          tile_rows=tile_rows)
+        assert torch.isfinite(out.float()).all()
+        _close(out, ref, atol=2e-2)
+
+
 def _sample_state(B, V, rows, base, maxnew, temp, dev="cuda"):
     return dict(
         fsm_base=torch.tensor(base, dtype=torch.int32, device=dev),

@@ -52,7 +52,7 @@ def gemms(cfg, M, mode):
     return res
 
 
-def attention(cfg, n_prompts, prompt, prefix):
+def attention(cfg, n_prompts, prompt, prefix, tile_rows=64):
     from byzantine_consensus_llm_agents_amd.ops import get_ops
     hip = get_ops("hip")
     bs, hd = 16, cfg.head_dim
@@ -66,20 +66,21 @@ def attention(cfg, n_prompts, prompt, prefix):
     q_start = torch.arange(n_prompts + 1, dtype=torch.int32) * prompt
     tiles = []
     for i in range(n_prompts):
-        for t in range(i * prompt, (i + 1) * prompt, 64):
-            tiles.append((i, t, min(t + 64, (i + 1) * prompt)))
+        for t in range(i * prompt, (i + 1) * prompt, tile_rows):
+            tiles.append((i, t, min(t + tile_rows, (i + 1) * prompt)))
     tiles.sort(key=lambda x: -(x[2] - x[0] * prompt))  # deepest first, as the engine orders them
     tiles = torch.tensor(tiles, dtype=torch.int32).cuda()
     T = n_prompts * prompt
     q = torch.randn(T, n_q, hd, device="cuda", dtype=torch.bfloat16)
     seq_lens = torch.full((n_prompts,), ctx, dtype=torch.int32, device="cuda")
     us = timeit(lambda: hip.paged_attention_prefill(q, k, v, 0, tables, q_start.cuda(), seq_lens, hd ** -0.5,
-                                                    prompt, tiles))
+                                                    prompt, tiles, tile_rows=tile_rows))
     # causal FLOPs: each query sees prefix + its causal part
     flops = 4 * n_q * hd * n_prompts * (prompt * prefix + prompt * (prompt + 1) / 2)
-    r = {"prompts": n_prompts, "prompt": prompt, "prefix": prefix, "us": round(us, 1),
+    r = {"prompts": n_prompts, "prompt": prompt, "prefix": prefix, "tile_rows": tile_rows, "us": round(us, 1),
          "tflops": round(flops / us / 1e6, 1)}
-    print(f"[attn] {n_prompts}x{prompt} (+{prefix} cached) {us:9.1f} us {r['tflops']:7.1f} TF/s", flush=True)
+    print(f"[attn rows={tile_rows}] {n_prompts}x{prompt} (+{prefix} cached) {us:9.1f} us {r['tflops']:7.1f} TF/s",
+          flush=True)
     return r
 
 
@@ -91,6 +92,9 @@ def main():
     ap.add_argument("--skip-gemm", action="store_true")
     ap.add_argument("--skip-attn", action="store_true")
     ap.add_argument("--attn-model", default=None, help="model geometry for the attention runs")
+    ap.add_argument("--tile-rows", default="64", help="prefill attention tile sizes to time (64,128,256)")
+    ap.add_argument("--attn-shapes", default="12x1024+512,16x900+400,8x2048+0",
+                    help="prompts x new tokens + cached prefix")
     args = ap.parse_args()
     cfg = get_model_config(args.model)
     out = {"model": cfg.name, "gemm": {}, "attention": []}
@@ -112,8 +116,14 @@ def main():
         torch.backends.cuda.preferred_blas_library("cublaslt")
         torch.cuda.tunable.enable(False)
     acfg = get_model_config(args.attn_model) if args.attn_model else cfg
-    for n, p, pre in (() if args.skip_attn else ((12, 1024, 512), (16, 900, 400), (8, 2048, 0))):
-        out["attention"].append(attention(acfg, n, p, pre))
+    shapes = []
+    for spec in args.attn_shapes.split(","):
+        n, rest = spec.split("x")
+        p, pre = rest.split("+")
+        shapes.append((int(n), int(p), int(pre)))
+    for n, p, pre in (() if args.skip_attn else shapes):
+        for tr in (int(x) for x in args.tile_rows.split(",")):
+            out["attention"].append(attention(acfg, n, p, pre, tr))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "bench_prefill.json"), "w") as fh:
         json.dump(out, fh, indent=1)
