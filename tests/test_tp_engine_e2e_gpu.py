@@ -79,12 +79,14 @@ def _play(rank, world, port, model, quant, honest, byz, out):
         sim = BCGSimulation(honest, byz, config={"max_rounds": ROUNDS, "value_range": (0, 50),
                                                  "consensus_threshold": 66.0, "verbose": False,
                                                  "byzantine_awareness": "may_exist", "seed": 99})
+        played = 0  # rounds run (a stop vote in round r leaves current_round at r)
         for _ in range(ROUNDS):
             if sim.game.game_over:
                 break
             sim.run_round()
+            played += 1
         st = sim.game.get_statistics()
-        res.update(counters=dict(sim.counters), rounds=min(sim.game.current_round - 1, ROUNDS),
+        res.update(counters=dict(sim.counters), rounds=played,
                    game_over=bool(sim.game.game_over),
                    outcome=st.get("consensus_outcome"), keys=sorted(st),
                    values={a: s.current_value for a, s in sim.game.agents.items()})
