@@ -1060,6 +1060,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef PREFILL32_KFIRST
 #define PREFILL32_KFIRST 1
 #endif
+#ifndef PREFILL32_PRIO
+#define PREFILL32_PRIO 0  // s_setprio 1 over the S^T MFMA block
+#endif
 #ifndef PREFILL32_SCHED
 #define PREFILL32_SCHED 0  // pin the LDS reads one step ahead of their MFMAs (sched_group_barrier)
 #endif
@@ -1088,11 +1091,18 @@ __device__ __forceinline__ void attn32_scores(const unsigned char* slot, int k_l
     ka[kk][1] = *reinterpret_cast<const bf16x8*>(p + 32 * 256);
   }
   __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler sinks them to their uses)
+#if PREFILL32_PRIO
+  __builtin_amdgcn_s_setprio(1);  // the MFMA block first when the SIMD's other wave is in its softmax
+#endif
 #pragma unroll
   for (int kk = 0; kk < 8; ++kk) {
     s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[kk][0], bq[kk], s0, 0, 0, 0);
     s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[kk][1], bq[kk], s1, 0, 0, 0);
   }
+#if PREFILL32_PRIO
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_setprio(0);
+#endif
 #else
   bf16x8 a0 = *reinterpret_cast<const bf16x8*>(slot + k_lane);
   bf16x8 a1 = *reinterpret_cast<const bf16x8*>(slot + k_lane + 32 * 256);
