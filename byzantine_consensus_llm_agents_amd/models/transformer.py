@@ -329,7 +329,7 @@ class DecoderModel:
         ops, c = self.ops, self.cfg
         q = ops.qk_norm_rope_kv_write(qkv, meta.positions, meta.slots, self.n_q, self.n_kv, self.hd,
                                       L.get("q_norm"), L.get("k_norm"), c.rms_eps, self.cos_sin,
-                                      k_cache, v_cache, li)
+                                      k_cache, v_cache, li, contiguous=not meta.decode)
         if meta.decode:
             lens = meta.seq_lens if meta.attn_seq_lens is None else meta.attn_seq_lens
             return ops.paged_attention_decode(q, k_cache, v_cache, li, meta.block_tables, lens,

@@ -65,7 +65,7 @@ def load_library(path: str = None) -> ctypes.CDLL:
         "bcg_embed_rmsnorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
         "bcg_qk_norm_rope_kv_write": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                                      c_float, c_int, c_void_p],
+                                      c_float, c_int, c_int, c_void_p],
         "bcg_paged_attention_decode": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
                                        c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int,
                                        c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
@@ -174,7 +174,9 @@ def hip_ops() -> SimpleNamespace:
         return out
 
     def qk_norm_rope_kv_write(qkv, positions, slots, n_q, n_kv, head_dim, q_norm, k_norm, eps, cos_sin,
-                              k_cache, v_cache, layer):
+                              k_cache, v_cache, layer, contiguous=True):
+        """contiguous: the tokens come in runs of consecutive slots (prefill chunks), so V can be
+        written a whole KV block at a time; False for decode batches (one token per sequence)."""
         T = qkv.shape[0]
         _req(qkv.is_contiguous() and qkv.shape[1] == (n_q + 2 * n_kv) * head_dim, "qkv shape")
         _req(positions.dtype == torch.int32 and slots.dtype == torch.int32 and positions.numel() == T
@@ -186,7 +188,8 @@ def hip_ops() -> SimpleNamespace:
         _check(lib.bcg_qk_norm_rope_kv_write(
             _p(qkv), _p(positions), _p(slots), _p(q), _p(q_norm) if q_norm is not None else None,
             _p(k_norm) if k_norm is not None else None, _p(cos_sin), _p(k_cache), _p(v_cache), layer, T,
-            n_q, n_kv, head_dim, NB, BS, eps, _kv_fp8(k_cache, v_cache), _stream()), "qk_norm_rope_kv_write")
+            n_q, n_kv, head_dim, NB, BS, eps, _kv_fp8(k_cache, v_cache), int(bool(contiguous)), _stream()),
+            "qk_norm_rope_kv_write")
         return q
 
     def decode_workspace_numel(B, n_q, hd, max_blocks, block_size=16, cascade=True):

@@ -63,7 +63,8 @@ def _rope(x: torch.Tensor, cs: torch.Tensor) -> torch.Tensor:
 def qk_norm_rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor,
                           n_q: int, n_kv: int, head_dim: int, q_norm: Optional[torch.Tensor],
                           k_norm: Optional[torch.Tensor], eps: float, cos_sin: torch.Tensor,
-                          k_cache: torch.Tensor, v_cache: torch.Tensor, layer: int) -> torch.Tensor:
+                          k_cache: torch.Tensor, v_cache: torch.Tensor, layer: int,
+                          contiguous: bool = True) -> torch.Tensor:
     """Split fused QKV, (Qwen3) RMSNorm q/k per head, neox RoPE, scatter K/V into the paged cache.
 
     Returns q as ``[T, n_q, head_dim]`` (activation dtype).

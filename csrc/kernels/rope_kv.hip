@@ -234,10 +234,13 @@ __global__ __launch_bounds__(2 * HD) void v_write_group_kernel(const bf16_t* __r
 template <typename CacheT, int HD>
 void launch_vec(const void* qkv, const int* positions, const int* slots, void* q_out, const void* q_norm,
                 const void* k_norm, const float* cos_sin, void* k_cache, void* v_cache, int layer, int T, int n_q,
-                int n_kv, int num_blocks, int block_size, float eps, hipStream_t stream) {
+                int n_kv, int num_blocks, int block_size, float eps, int contiguous, hipStream_t stream) {
   constexpr int HPB = 4 * (64 / (HD / 8));  // heads per 256-thread block
   const int n_heads = n_q + 2 * n_kv;
-  const bool group_v = std::is_same<CacheT, bf16_t>::value && T >= 64;
+  // contiguous = 0 (decode: one token per sequence): no group ever fills a block, and the grouped
+  // writer's element-wise path walked its 16 tokens one after another (13.6 us per layer at 768
+  // rows against ~1 us of transposed stores inside the rope kernel)
+  const bool group_v = std::is_same<CacheT, bf16_t>::value && T >= 64 && contiguous;
   // group_v: v_write_group_kernel stores V, so the grid covers the query/key heads only (a
   // block past them would load its V rows just to return: Qwen3-14B's fourth head block, 2 KB
   // per token); V heads inside the last query/key block still return early through skip_v
@@ -261,23 +264,23 @@ BCG_API int bcg_qk_norm_rope_kv_write(const void* qkv, const int* positions, con
                                       const void* q_norm, const void* k_norm, const float* cos_sin,
                                       void* k_cache, void* v_cache, int layer, int T, int n_q, int n_kv,
                                       int hd, int num_blocks, int block_size, float eps, int kv_fp8,
-                                      hipStream_t stream) {
+                                      int contiguous, hipStream_t stream) {
   if (hd > 128 || (hd & 1) || T <= 0) return -2;
   if (hd == 128 || hd == 64) {
     if (kv_fp8) {
       if (hd == 128)
         launch_vec<uint8_t, 128>(qkv, positions, slots, q_out, q_norm, k_norm, cos_sin, k_cache, v_cache, layer, T,
-                                 n_q, n_kv, num_blocks, block_size, eps, stream);
+                                 n_q, n_kv, num_blocks, block_size, eps, contiguous, stream);
       else
         launch_vec<uint8_t, 64>(qkv, positions, slots, q_out, q_norm, k_norm, cos_sin, k_cache, v_cache, layer, T,
-                                n_q, n_kv, num_blocks, block_size, eps, stream);
+                                n_q, n_kv, num_blocks, block_size, eps, contiguous, stream);
     } else {
       if (hd == 128)
         launch_vec<bf16_t, 128>(qkv, positions, slots, q_out, q_norm, k_norm, cos_sin, k_cache, v_cache, layer, T,
-                                n_q, n_kv, num_blocks, block_size, eps, stream);
+                                n_q, n_kv, num_blocks, block_size, eps, contiguous, stream);
       else
         launch_vec<bf16_t, 64>(qkv, positions, slots, q_out, q_norm, k_norm, cos_sin, k_cache, v_cache, layer, T,
-                               n_q, n_kv, num_blocks, block_size, eps, stream);
+                               n_q, n_kv, num_blocks, block_size, eps, contiguous, stream);
     }
     return BCG_CHECK_LAUNCH();
   }

@@ -97,6 +97,10 @@ def test_qk_norm_rope_kv_write_prefill_groups(hip, hd, n_q, n_kv):
     _close(q, q_ref, atol=3e-2)
     _close(k2, k1, atol=3e-2)
     assert torch.equal(v2, v1)
+    # the same tokens flagged non-contiguous (decode batches): V written by the rope kernel itself
+    k3, v3 = _caches(L, NB, n_kv, hd, fill=False)
+    q3 = hip.qk_norm_rope_kv_write(qkv, pos, slots, n_q, n_kv, hd, qn, kn, 1e-6, cs, k3, v3, 1, contiguous=False)
+    assert torch.equal(q3, q) and torch.equal(k3, k2) and torch.equal(v3, v1)
 
 
 def _tables(B, lens, NB, max_blocks, gen):
