@@ -368,7 +368,8 @@ class InferenceEngine:
             self.cascade = CascadeTables(cap, dev, self.args.kv_block_size)
         self._layout_dirty = True  # live rows changed since the cascade tables were built
         rows_fn = getattr(self.ops, "prefill_tile_rows", None)
-        self._tile_rows = rows_fn(self.model.hd, self.kv_dtype() == torch.float8_e4m3fn) if rows_fn else 64
+        self._tile_rows = (rows_fn(self.model.hd, self.kv_dtype() == torch.float8_e4m3fn, self.max_blocks_per_seq)
+                           if rows_fn else 64)
 
     def _phys(self, blocks: List[int]) -> List[int]:
         return [b + 1 for b in blocks]  # manager ids are shifted past scratch block 0

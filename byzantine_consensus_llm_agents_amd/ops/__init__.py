@@ -32,7 +32,7 @@ def _torch_ops() -> SimpleNamespace:
         qk_norm_rope_kv_write=_ref.qk_norm_rope_kv_write,
         paged_attention_decode=decode,
         paged_attention_prefill=prefill,
-        prefill_tile_rows=lambda hd, kv_fp8=False: 64,
+        prefill_tile_rows=lambda hd, kv_fp8=False, max_blocks=0: 64,
         silu_mul=_ref.silu_mul,
         linear_silu=_ref.linear_silu,
         linear_residual=_ref.linear_residual,

@@ -18,6 +18,7 @@ from ..utils.build import kernel_sources, kernels_source_hash, kernels_target
 _LIB = None
 # Rows per prefill attention tile unless BCG_PREFILL_TILE_ROWS says otherwise (prefill_tile_rows)
 PREFILL_TILE_ROWS = 128
+PREFILL32_MAX_BLOCKS = 1024  # csrc/kernels/attention.hip: the 32x32 kernel's LDS block-id table
 
 c_int, c_float, c_void_p, c_uint32, c_int64 = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int64
 
@@ -263,12 +264,14 @@ def hip_ops() -> SimpleNamespace:
             4, _kv_fp8(k_cache, v_cache), _stream()), "paged_attention_prefill")
         return out
 
-    def prefill_tile_rows(hd, kv_fp8=False):
+    def prefill_tile_rows(hd, kv_fp8=False, max_blocks=0):
         """Rows per prefill attention tile for this geometry (the tile table the caller builds):
-        128 / 256 select the LDS-staged 32x32 kernel (head dim 128, bf16 KV), 64 the 16x16 one.
+        128 / 256 select the LDS-staged 32x32 kernel (head dim 128, bf16 KV, block tables of at
+        most 1024 entries -- 16k tokens -- which it stages in LDS), 64 the 16x16 one.
         BCG_PREFILL_TILE_ROWS overrides the default."""
         rows = int(os.environ.get("BCG_PREFILL_TILE_ROWS", PREFILL_TILE_ROWS))
-        return rows if rows in (128, 256) and hd == 128 and not kv_fp8 else 64
+        ok = rows in (128, 256) and hd == 128 and not kv_fp8 and max_blocks <= PREFILL32_MAX_BLOCKS
+        return rows if ok else 64
 
     # Per-call GEMM dispatch log (VERDICT r3: which projection shapes reach a hand kernel, also
     # inside TP worker processes that no profiler sees): (M, N, K, epi, dtype) -> choice -> calls.

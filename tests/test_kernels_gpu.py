@@ -231,6 +231,7 @@ def test_paged_attention_prefill32(hip, n_q, n_kv, tile_rows):
             tiles.append((i, t, min(t + tile_rows, q_start[i + 1])))
     tiles = torch.tensor(tiles[::-1], dtype=torch.int32, device="cuda")
     assert hip.prefill_tile_rows(hd) in (64, 128, 256) and hip.prefill_tile_rows(64) == 64
+    assert hip.prefill_tile_rows(hd, max_blocks=2048) == 64  # longer tables than the kernel stages
     for _ in range(2):  # repeated launches: the LDS ring starts clean every time
         out = hip.paged_attention_prefill(q, k, v, layer, tables, qs, seq, hd ** -0.5, None, tiles,
                                           tile_rows=tile_rows)
