@@ -1060,6 +1060,18 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef PREFILL32_KFIRST
 #define PREFILL32_KFIRST 1
 #endif
+#ifndef PREFILL32_REGSTAGE
+#define PREFILL32_REGSTAGE 0  // 1: K/V staged through VGPRs + ds_write (measured: no faster than the LDS-DMA)
+#endif
+#ifndef PREFILL32_ASM_DMA
+#define PREFILL32_ASM_DMA 1  // the LDS-DMA as inline asm (see issue() in the kernel)
+#endif
+#ifndef PREFILL32_DMA_SPLIT
+#define PREFILL32_DMA_SPLIT 0
+#endif
+#ifndef PREFILL32_XCD
+#define PREFILL32_XCD 1  // XCD-grouped 1-D grid (0: grid (tiles, heads))
+#endif
 #ifndef PREFILL32_PRIO
 #define PREFILL32_PRIO 0  // s_setprio 1 over the S^T MFMA block
 #endif
@@ -1131,6 +1143,9 @@ __device__ __forceinline__ void attn32_scores(const unsigned char* slot, int k_l
     for (int i = 0; i < 32; ++i)
       if (rel_pos + 32 * (i >> 4) + 16 * ((i >> 3) & 1) + (i & 7) > 0) t[i] = -INFINITY;
   }
+#ifdef PREFILL32_ABL_NOSOFTMAX  // timing ablation only (wrong results): no max / rescale / scaling
+  return;
+#endif
   float v = t[0];
 #pragma unroll
   for (int i = 1; i < 31; i += 2) v = vmax3(v, t[i], t[i + 1]);
@@ -1167,7 +1182,11 @@ __device__ __forceinline__ void attn32_pv(const unsigned char* slot, int v_lane,
   f32x2 ps = {0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < 32; i += 2) {
+#ifdef PREFILL32_ABL_NOSOFTMAX
+    const f32x2 p = {t[i], t[i + 1]};
+#else
     const f32x2 p = {fast_exp2(t[i]), fast_exp2(t[i + 1])};
+#endif
     ps += p;
     bp[i >> 3][i & 7] = static_cast<__bf16>(p.x);
     bp[i >> 3][(i & 7) + 1] = static_cast<__bf16>(p.y);
@@ -1210,7 +1229,7 @@ template <int NW, int NS>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void prefill_attn32_kernel(
     const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
     const int* __restrict__ q_start, const int* __restrict__ seq_lens, const int* __restrict__ tiles, int n_q,
-    float scale_log2, bf16_t* __restrict__ out) {
+    float scale_log2, bf16_t* __restrict__ out, int n_tiles) {
   constexpr int HD = 128, KC = 64;                   // head dim, tokens per chunk
   constexpr int KBYTES = KC * HD * 2, SLOT = 2 * KBYTES;  // K (then V) image of one chunk: 16 KiB each
   constexpr int P = 32 / NW;                         // 1-KiB DMA pieces per wave per chunk
@@ -1218,7 +1237,22 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   static_assert(NS >= 2 && NS <= 4, "ring depth");
   __shared__ __attribute__((aligned(1024))) unsigned char ring[NS * SLOT];
 
-  const int tile = blockIdx.x, qh = blockIdx.y;
+  // XCD-grouped order (1-D grid): workgroup id i runs on XCD i % 8, so kv head i % n_kv puts every
+  // query head of a kv head on the same XCD(s) (one XCD per kv head at n_kv = 8), the G heads of
+  // one tile next to each other: the K/V chunks they all stage come from that XCD's L2
+  int tile, qh;
+#if PREFILL32_XCD
+  {
+    const int G = n_q / g.n_kv, kv = blockIdx.x % g.n_kv, rest = blockIdx.x / g.n_kv;
+    tile = rest / G;
+    qh = kv * G + rest % G;
+    if (tile >= n_tiles) return;
+  }
+#else
+  tile = blockIdx.x;
+  qh = blockIdx.y;
+  (void)n_tiles;
+#endif
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 31, h = lane >> 5;
   const int b = tiles[3 * tile], q_begin = tiles[3 * tile + 1], q_end = tiles[3 * tile + 2];
@@ -1250,24 +1284,76 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   // chunk (lane & 15) ^ row; V^T piece rows d = 32 (i & 3) + lane / 2, half (lane & 1) ^ bit 3 of d)
   const int lane_kx = (lane & 15) ^ (lane >> 4), lane_k = (lane >> 4) * 256;
   const int lane_v = (lane >> 1) * 32 + (((lane ^ (lane >> 4)) & 1) << 4);
-  auto issue = [&](int c) __attribute__((always_inline)) {
+  auto issue = [&](int c, int p0 = 0, int p1 = 1 << 30) __attribute__((always_inline)) {
+#ifdef PREFILL32_ABL_NODMA  // timing ablation only (wrong results): K / V never staged
+    return;
+#endif
     unsigned char* slot = ring + (c % NS) * SLOT;
     int blk[P];
 #pragma unroll
     for (int pi = 0; pi < P; ++pi) blk[pi] = blk_ids[4 * c + (((w * P + pi) & 15) >> 2)];
+#ifdef PREFILL32_ABL_HOTSRC  // timing ablation only (wrong results): every chunk re-reads chunk 0 (L2-hot)
+#pragma unroll
+    for (int pi = 0; pi < P; ++pi) blk[pi] = blk_ids[((w * P + pi) & 15) >> 2];
+#endif
 #pragma unroll
     for (int pi = 0; pi < P; ++pi) {
+      if (pi < p0 || pi >= p1) continue;  // compile-time after inlining
       const int i = w * P + pi;  // piece 0..31, wave-uniform
       const int r4 = i & 3;
       const size_t base = ((head_base + __builtin_amdgcn_readfirstlane(blk[pi])) * g.n_kv + kvh) * (BS * HD * 2);
+#if PREFILL32_ASM_DMA
+      // The DMA as inline asm (M0 = the piece's LDS address): hipcc tracks the builtin's LDS write
+      // and put a vmcnt(0) before the next ds_read of the ring -- every chunk then waited for its
+      // successor's pieces to land (the whole fetch latency exposed once per chunk).  The ring's
+      // own counted wait + barrier in sync() orders the reads.
+      const unsigned char* src = i < 16 ? kc + base + (r4 * 1024 + lane_k + ((lane_kx ^ (4 * r4)) << 4))
+                                        : vc + base + (r4 * 1024 + lane_v);
+      const uint32_t m0v = __builtin_amdgcn_readfirstlane(
+          static_cast<uint32_t>(reinterpret_cast<uintptr_t>(slot + (i < 16 ? i * 1024 : KBYTES + (i - 16) * 1024))));
+      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(src), "s"(m0v) : "memory", "m0");
+#else
       if (i < 16)  // K rows 4i .. 4i+3 of the chunk
         __builtin_amdgcn_global_load_lds(kc + base + (r4 * 1024 + lane_k + ((lane_kx ^ (4 * r4)) << 4)),
                                          slot + i * 1024, 16, 0, 0);
       else  // V^T rows 32 (i & 3) .. + 31 of block (i & 15) / 4
         __builtin_amdgcn_global_load_lds(vc + base + (r4 * 1024 + lane_v), slot + KBYTES + (i - 16) * 1024, 16,
                                          0, 0);
+#endif
     }
   };
+
+#if PREFILL32_REGSTAGE
+  // Register staging: this wave's P pieces of chunk c + 2 are loaded into VGPRs (plain 16-B
+  // loads; the source-side swizzle as above) while chunk c computes, and written into the ring
+  // with ds_write_b128 after the next barrier.  LDS-DMA fills run at ~25 GB/s per CU (the
+  // chip-wide ~6.4 TB/s of MI355X_MICROARCH's ldsdma-fill row) even from L2, about half of
+  // what this kernel consumes at its MFMA rate; a kernel without the DMA (timing ablation)
+  // ran 2.1-2.3x faster.
+  u32x4 stg[P];
+  auto load_regs = [&](int c) __attribute__((always_inline)) {
+    int blk[P];
+#pragma unroll
+    for (int pi = 0; pi < P; ++pi) blk[pi] = blk_ids[4 * c + (((w * P + pi) & 15) >> 2)];
+#pragma unroll
+    for (int pi = 0; pi < P; ++pi) {
+      const int i = w * P + pi;
+      const int r4 = i & 3;
+      const size_t base = ((head_base + __builtin_amdgcn_readfirstlane(blk[pi])) * g.n_kv + kvh) * (BS * HD * 2);
+      const unsigned char* src = i < 16 ? kc + base + (r4 * 1024 + lane_k + ((lane_kx ^ (4 * r4)) << 4))
+                                        : vc + base + (r4 * 1024 + lane_v);
+      stg[pi] = *reinterpret_cast<const u32x4*>(src);
+    }
+  };
+  auto write_regs = [&](int c) __attribute__((always_inline)) {
+    unsigned char* slot = ring + (c % NS) * SLOT + lane * 16;
+#pragma unroll
+    for (int pi = 0; pi < P; ++pi) {
+      const int i = w * P + pi;
+      *reinterpret_cast<u32x4*>(slot + (i < 16 ? i * 1024 : KBYTES + (i - 16) * 1024)) = stg[pi];
+    }
+  };
+#endif
 
   // Q^T operands: lane (col, h) holds dims 16 kk + 8 h .. + 7 of its row
   bf16x8 bq[HD / 16];
@@ -1285,9 +1371,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     }
   }
   __syncthreads();  // block ids staged
+#if PREFILL32_REGSTAGE
+  (void)issue;
+  load_regs(0);
+  write_regs(0);
+  if (1 < nchunk) load_regs(1);
+#else
 #pragma unroll
   for (int c = 0; c < NS - 1; ++c)
     if (c < nchunk) issue(c);
+#endif
 
   // K operand addresses: S^T row m = col holds token t0(m) (tile u = 0; u = 1 is t0 + 32, the same
   // swizzle); 16-B chunk 2 kk + h of that row sits at slot (2 kk + h) ^ (t0 & 15), i.e. at byte
@@ -1303,6 +1396,31 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
 
   // chunk c's pieces landed and its successor's slot is free: wait + barrier, then the DMA of
   // chunk c + NS - 1 (every wave runs this for every chunk of the workgroup)
+#if PREFILL32_REGSTAGE
+  // chunk c's image complete (every wave's writes) and every wave past chunk c - 1
+  auto sync = [&](int c) __attribute__((always_inline)) {
+    (void)c;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // after the S^T MFMAs: chunk c + 1 into the slot chunk c - 1 used, chunk c + 2's loads issued
+  auto stage = [&](int c) __attribute__((always_inline)) {
+    if (c + 1 < nchunk) {
+      write_regs(c + 1);
+      if (c + 2 < nchunk) load_regs(c + 2);
+    }
+  };
+#else
+  // PREFILL32_DMA_SPLIT (NS = 2): half of the next chunk's pieces right after the barrier, the
+  // other half after the S^T MFMAs, instead of all eight in one burst
+  auto stage = [&](int c) __attribute__((always_inline)) {
+    if constexpr (PREFILL32_DMA_SPLIT && NS == 2) {
+      if (c + 1 < nchunk) issue(c + 1, P / 2, P);
+    } else {
+      (void)c;
+    }
+  };
   auto sync = [&](int c) __attribute__((always_inline)) {
     const int ahead = min(NS - 2, nchunk - 1 - c);  // later chunks whose pieces may still fly
 #ifndef PREFILL32_ABL_NOWAIT  // timing ablation only (wrong results): the DMA is never waited for
@@ -1318,8 +1436,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
 #endif
     __builtin_amdgcn_s_barrier();  // ... and every wave is past chunk c - 1: its slot is free
     asm volatile("" ::: "memory");
-    if (c + NS - 1 < nchunk) issue(c + NS - 1);
+    if (c + NS - 1 < nchunk) {
+      if constexpr (PREFILL32_DMA_SPLIT && NS == 2)
+        issue(c + NS - 1, 0, P / 2);
+      else
+        issue(c + NS - 1);
+    }
   };
+#endif
   auto slot_of = [&](int c) { return static_cast<const unsigned char*>(ring + (c % NS) * SLOT); };
   int c = 0;
   float t[32];
@@ -1328,14 +1452,19 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   for (; c < n_full; ++c) {
     sync(c);
     attn32_scores<false>(slot_of(c), k_lane, bq, scale_log2, 0, m, lsum, o, t);
+    stage(c);
     attn32_pv<false>(slot_of(c), v_lane, 0, t, lsum, o);
   }
   for (; c < w_chunks; ++c) {
     sync(c);
     attn32_scores<true>(slot_of(c), k_lane, bq, scale_log2, c * KC + 8 * h - pos_q, m, lsum, o, t);
+    stage(c);
     attn32_pv<true>(slot_of(c), v_lane, c * KC + 8 * h - ctx, t, lsum, o);
   }
-  for (; c < nchunk; ++c) sync(c);  // chunks in the causal future of every row of this wave
+  for (; c < nchunk; ++c) {  // chunks in the causal future of every row of this wave
+    sync(c);
+    stage(c);
+  }
   if (!active || row0 + col >= q_end) return;
   {
     const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum), __float_as_uint(lsum), false, false);
@@ -1463,19 +1592,23 @@ BCG_API int bcg_paged_attention_prefill32(const void* q, const void* k_cache, co
                                           int n_q, int hd, int block_size, float scale, void* out, int tile_rows,
                                           int kv_fp8, hipStream_t stream) {
   if (block_size != BS || n_kv <= 0 || n_q % n_kv || n_tiles <= 0 || n_q > 65535 || hd != 128 || kv_fp8 ||
-      max_blocks > PREFILL32_MAX_BLOCKS)
+      max_blocks > PREFILL32_MAX_BLOCKS || static_cast<long long>(n_tiles) * n_q > 0x7fffffffLL)
     return -2;
   KVGeom g{static_cast<const bf16_t*>(k_cache), static_cast<const bf16_t*>(v_cache), layer, num_blocks, n_kv};
   const float sl = scale * LOG2E;
   const bf16_t* qb = static_cast<const bf16_t*>(q);
   bf16_t* ob = static_cast<bf16_t*>(out);
+#if PREFILL32_XCD
+  const dim3 grid(n_tiles * n_q);
+#else
   const dim3 grid(n_tiles, n_q);
+#endif
   if (tile_rows == 128)
     hipLaunchKernelGGL((prefill_attn32_kernel<4, PREFILL32_NS4>), grid, dim3(256), 0, stream, qb, g, block_tables,
-                       max_blocks, q_start, seq_lens, tiles, n_q, sl, ob);
+                       max_blocks, q_start, seq_lens, tiles, n_q, sl, ob, n_tiles);
   else if (tile_rows == 256)
     hipLaunchKernelGGL((prefill_attn32_kernel<8, PREFILL32_NS8>), grid, dim3(512), 0, stream, qb, g, block_tables,
-                       max_blocks, q_start, seq_lens, tiles, n_q, sl, ob);
+                       max_blocks, q_start, seq_lens, tiles, n_q, sl, ob, n_tiles);
   else
     return -2;
   return BCG_CHECK_LAUNCH();
