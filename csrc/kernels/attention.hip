@@ -1063,6 +1063,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef PREFILL32_REGSTAGE
 #define PREFILL32_REGSTAGE 0  // 1: K/V staged through VGPRs + ds_write (measured: no faster than the LDS-DMA)
 #endif
+#ifndef PREFILL32_HP2
+#define PREFILL32_HP2 0  // 128-row tiles: two query heads per 8-wave workgroup (measured slower: profiles/r6_prefill32)
+#endif
 #ifndef PREFILL32_ASM_DMA
 #define PREFILL32_ASM_DMA 1  // the LDS-DMA as inline asm (see issue() in the kernel)
 #endif
@@ -1225,46 +1228,66 @@ __device__ __forceinline__ void attn32_pv(const unsigned char* slot, int v_lane,
   }
 }
 
-template <int NW, int NS>
+// HP = 2 (8 waves): the workgroup serves query heads 2p and 2p + 1 of the same 128-row tile
+// (4 waves each) and stages each chunk ONCE for both when they share a kv head -- half the staged
+// bytes per FLOP of HP = 1 -- or one image per kv head when the pair straddles two (G odd).
+template <int NW, int NS, int HP = 1>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void prefill_attn32_kernel(
     const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
     const int* __restrict__ q_start, const int* __restrict__ seq_lens, const int* __restrict__ tiles, int n_q,
     float scale_log2, bf16_t* __restrict__ out, int n_tiles) {
   constexpr int HD = 128, KC = 64;                   // head dim, tokens per chunk
   constexpr int KBYTES = KC * HD * 2, SLOT = 2 * KBYTES;  // K (then V) image of one chunk: 16 KiB each
-  constexpr int P = 32 / NW;                         // 1-KiB DMA pieces per wave per chunk
+  constexpr int RW = NW / HP;                        // waves (32-row groups) per head
+  constexpr int P = 32 * HP / NW;                    // 1-KiB DMA pieces per wave per chunk (all images)
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(HP == 1 || (HP == 2 && NW == 8), "head pairs need 8 waves");
   static_assert(NS >= 2 && NS <= 4, "ring depth");
-  __shared__ __attribute__((aligned(1024))) unsigned char ring[NS * SLOT];
+  static_assert(HP == 1 || !PREFILL32_REGSTAGE, "register staging is built for one head per workgroup");
+  __shared__ __attribute__((aligned(1024))) unsigned char ring[NS * SLOT * HP];
 
   // XCD-grouped order (1-D grid): workgroup id i runs on XCD i % 8, so kv head i % n_kv puts every
   // query head of a kv head on the same XCD(s) (one XCD per kv head at n_kv = 8), the G heads of
   // one tile next to each other: the K/V chunks they all stage come from that XCD's L2
-  int tile, qh;
+  const int G = n_q / g.n_kv;
+  int tile, qa;  // qa: the workgroup's (first) query head
 #if PREFILL32_XCD
-  {
-    const int G = n_q / g.n_kv, kv = blockIdx.x % g.n_kv, rest = blockIdx.x / g.n_kv;
+  if constexpr (HP == 1) {
+    const int kv = blockIdx.x % g.n_kv, rest = blockIdx.x / g.n_kv;
     tile = rest / G;
-    qh = kv * G + rest % G;
-    if (tile >= n_tiles) return;
+    qa = kv * G + rest % G;
+  } else {  // the head pairs whose first head belongs to kv head kv: pairs [ceil(kv G / 2), ceil((kv + 1) G / 2))
+    constexpr int HPP = HP;
+    const int ppk = (G + HPP - 1) / HPP, kv = blockIdx.x % g.n_kv, rest = blockIdx.x / g.n_kv;
+    tile = rest / ppk;
+    const int p = (kv * G + 1) / 2 + rest % ppk;
+    if (p >= ((kv + 1) * G + 1) / 2) return;  // this kv head owns fewer pairs
+    qa = 2 * p;
   }
+  if (tile >= n_tiles) return;
 #else
   tile = blockIdx.x;
-  qh = blockIdx.y;
+  qa = HP * blockIdx.y;
   (void)n_tiles;
 #endif
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 31, h = lane >> 5;
+  const int hsel = w / RW;                            // which head of the workgroup this wave serves
+  const int qb = qa + 1 < n_q ? qa + 1 : qa;          // HP = 2: the second head (clamped; idle if none)
+  const int qh = hsel ? qb : qa;
+  const int kva = qa / G, kvb = qb / G;
+  const int n_img = (HP == 2 && kvb != kva) ? 2 : 1;  // K/V images staged per chunk
+  const int kvh = qh / G;
+  const int img = kvh != kva ? 1 : 0;                 // the image this wave reads
   const int b = tiles[3 * tile], q_begin = tiles[3 * tile + 1], q_end = tiles[3 * tile + 2];
   const int ctx = seq_lens[b];
   const int pos0 = ctx - (q_start[b + 1] - q_start[b]) - q_start[b];  // position of packed row r = pos0 + r
-  const int kvh = qh / (n_q / g.n_kv);
   const int* table = block_tables + static_cast<size_t>(b) * max_blocks;
   const int nblk = (ctx + BS - 1) / BS;
-  const int wg_last = min(q_begin + 32 * NW, q_end) - 1;
+  const int wg_last = min(q_begin + 32 * RW, q_end) - 1;
   const int nchunk = (pos0 + wg_last + KC) / KC;      // chunks the workgroup stages (uniform)
-  const int row0 = q_begin + 32 * w;
-  const bool active = row0 < q_end;                   // wave-uniform
+  const int row0 = q_begin + 32 * (w % RW);
+  const bool active = row0 < q_end && !(HP == 2 && hsel == 1 && qa + 1 >= n_q);  // wave-uniform
   const int w_last = min(row0 + 31, q_end - 1);
   const int w_chunks = active ? (pos0 + w_last + KC) / KC : 0;          // chunks this wave computes
   const int n_full = active ? min((pos0 + row0 + 1) / KC, w_chunks) : 0;  // ... seen in full by all its rows
@@ -1288,7 +1311,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
 #ifdef PREFILL32_ABL_NODMA  // timing ablation only (wrong results): K / V never staged
     return;
 #endif
-    unsigned char* slot = ring + (c % NS) * SLOT;
+    unsigned char* slot = ring + (c % NS) * (SLOT * HP);
     int blk[P];
 #pragma unroll
     for (int pi = 0; pi < P; ++pi) blk[pi] = blk_ids[4 * c + (((w * P + pi) & 15) >> 2)];
@@ -1299,9 +1322,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
 #pragma unroll
     for (int pi = 0; pi < P; ++pi) {
       if (pi < p0 || pi >= p1) continue;  // compile-time after inlining
-      const int i = w * P + pi;  // piece 0..31, wave-uniform
+      const int ig = w * P + pi;  // piece of all images, wave-uniform
+      const int im = ig >> 5, i = ig & 31;  // image, piece 0..31 of it
+      if (im >= n_img) continue;
       const int r4 = i & 3;
-      const size_t base = ((head_base + __builtin_amdgcn_readfirstlane(blk[pi])) * g.n_kv + kvh) * (BS * HD * 2);
+      const size_t base =
+          ((head_base + __builtin_amdgcn_readfirstlane(blk[pi])) * g.n_kv + (im ? kvb : kva)) * (BS * HD * 2);
 #if PREFILL32_ASM_DMA
       // The DMA as inline asm (M0 = the piece's LDS address): hipcc tracks the builtin's LDS write
       // and put a vmcnt(0) before the next ds_read of the ring -- every chunk then waited for its
@@ -1309,16 +1335,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
       // own counted wait + barrier in sync() orders the reads.
       const unsigned char* src = i < 16 ? kc + base + (r4 * 1024 + lane_k + ((lane_kx ^ (4 * r4)) << 4))
                                         : vc + base + (r4 * 1024 + lane_v);
-      const uint32_t m0v = __builtin_amdgcn_readfirstlane(
-          static_cast<uint32_t>(reinterpret_cast<uintptr_t>(slot + (i < 16 ? i * 1024 : KBYTES + (i - 16) * 1024))));
+      const uint32_t m0v = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(
+          reinterpret_cast<uintptr_t>(slot + im * SLOT + (i < 16 ? i * 1024 : KBYTES + (i - 16) * 1024))));
       asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(src), "s"(m0v) : "memory", "m0");
 #else
       if (i < 16)  // K rows 4i .. 4i+3 of the chunk
         __builtin_amdgcn_global_load_lds(kc + base + (r4 * 1024 + lane_k + ((lane_kx ^ (4 * r4)) << 4)),
-                                         slot + i * 1024, 16, 0, 0);
+                                         slot + im * SLOT + i * 1024, 16, 0, 0);
       else  // V^T rows 32 (i & 3) .. + 31 of block (i & 15) / 4
-        __builtin_amdgcn_global_load_lds(vc + base + (r4 * 1024 + lane_v), slot + KBYTES + (i - 16) * 1024, 16,
-                                         0, 0);
+        __builtin_amdgcn_global_load_lds(vc + base + (r4 * 1024 + lane_v),
+                                         slot + im * SLOT + KBYTES + (i - 16) * 1024, 16, 0, 0);
 #endif
     }
   };
@@ -1444,7 +1470,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     }
   };
 #endif
-  auto slot_of = [&](int c) { return static_cast<const unsigned char*>(ring + (c % NS) * SLOT); };
+  auto slot_of = [&](int c) { return static_cast<const unsigned char*>(ring + (c % NS) * (SLOT * HP) + img * SLOT); };
   int c = 0;
   float t[32];
   // chunks every row of the wave sees in full, then the diagonal (and context-end) chunks --
@@ -1600,10 +1626,15 @@ BCG_API int bcg_paged_attention_prefill32(const void* q, const void* k_cache, co
   bf16_t* ob = static_cast<bf16_t*>(out);
 #if PREFILL32_XCD
   const dim3 grid(n_tiles * n_q);
+  const dim3 grid2(n_tiles * n_kv * ((n_q / n_kv + 1) / 2));  // head pairs: ceil(G / 2) slots per kv head
 #else
   const dim3 grid(n_tiles, n_q);
+  const dim3 grid2(n_tiles, (n_q + 1) / 2);
 #endif
-  if (tile_rows == 128)
+  if (tile_rows == 128 && PREFILL32_HP2)
+    hipLaunchKernelGGL((prefill_attn32_kernel<8, 2, 2>), grid2, dim3(512), 0, stream, qb, g, block_tables, max_blocks,
+                       q_start, seq_lens, tiles, n_q, sl, ob, n_tiles);
+  else if (tile_rows == 128)
     hipLaunchKernelGGL((prefill_attn32_kernel<4, PREFILL32_NS4>), grid, dim3(256), 0, stream, qb, g, block_tables,
                        max_blocks, q_start, seq_lens, tiles, n_q, sl, ob, n_tiles);
   else if (tile_rows == 256)
