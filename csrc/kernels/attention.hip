@@ -1057,30 +1057,6 @@ void launch_prefill(int n_tiles, int n_q, const bf16_t* q, KVGeom g, const int* 
 //   V: block s at 16 KiB + s * 4 KiB, row d at d * 32, 16-B half e stored at e ^ ((d >> 3) & 1).
 // The source side of each LDS-DMA lane applies the swizzle (LDS destinations are consecutive).
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-#ifndef PREFILL32_KFIRST
-#define PREFILL32_KFIRST 1
-#endif
-#ifndef PREFILL32_REGSTAGE
-#define PREFILL32_REGSTAGE 0  // 1: K/V staged through VGPRs + ds_write (measured: no faster than the LDS-DMA)
-#endif
-#ifndef PREFILL32_HP2
-#define PREFILL32_HP2 0  // 128-row tiles: two query heads per 8-wave workgroup (measured slower: profiles/r6_prefill32)
-#endif
-#ifndef PREFILL32_ASM_DMA
-#define PREFILL32_ASM_DMA 1  // the LDS-DMA as inline asm (see issue() in the kernel)
-#endif
-#ifndef PREFILL32_DMA_SPLIT
-#define PREFILL32_DMA_SPLIT 0
-#endif
-#ifndef PREFILL32_XCD
-#define PREFILL32_XCD 1  // XCD-grouped 1-D grid (0: grid (tiles, heads))
-#endif
-#ifndef PREFILL32_PRIO
-#define PREFILL32_PRIO 0  // s_setprio 1 over the S^T MFMA block
-#endif
-#ifndef PREFILL32_SCHED
-#define PREFILL32_SCHED 0  // pin the LDS reads one step ahead of their MFMAs (sched_group_barrier)
-#endif
 constexpr int PREFILL32_MAX_BLOCKS = 1024;  // block-table width the 32x32 kernel stages in LDS (16k tokens)
 
 // One 64-token chunk of prefill_attn32_kernel for one wave (32 query columns):
@@ -1097,7 +1073,6 @@ __device__ __forceinline__ void attn32_scores(const unsigned char* slot, int k_l
                                               float scale_log2, int rel_pos, float& m, float& lsum,
                                               f32x16 (&o)[4], float (&t)[32]) {
   f32x16 s0 = f32x16{}, s1 = f32x16{};
-#if PREFILL32_KFIRST  // every K operand of the chunk read before the first MFMA (64 VGPRs, counted waits)
   bf16x8 ka[8][2];
 #pragma unroll
   for (int kk = 0; kk < 8; ++kk) {
@@ -1106,35 +1081,11 @@ __device__ __forceinline__ void attn32_scores(const unsigned char* slot, int k_l
     ka[kk][1] = *reinterpret_cast<const bf16x8*>(p + 32 * 256);
   }
   __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler sinks them to their uses)
-#if PREFILL32_PRIO
-  __builtin_amdgcn_s_setprio(1);  // the MFMA block first when the SIMD's other wave is in its softmax
-#endif
 #pragma unroll
   for (int kk = 0; kk < 8; ++kk) {
     s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[kk][0], bq[kk], s0, 0, 0, 0);
     s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[kk][1], bq[kk], s1, 0, 0, 0);
   }
-#if PREFILL32_PRIO
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_setprio(0);
-#endif
-#else
-  bf16x8 a0 = *reinterpret_cast<const bf16x8*>(slot + k_lane);
-  bf16x8 a1 = *reinterpret_cast<const bf16x8*>(slot + k_lane + 32 * 256);
-#pragma unroll
-  for (int kk = 0; kk < 8; ++kk) {  // the next k-step's K operands are read before this one's MFMAs
-    bf16x8 n0 = a0, n1 = a1;
-    if (kk + 1 < 8) {
-      const unsigned char* ka = slot + (k_lane ^ ((kk + 1) << 5));
-      n0 = *reinterpret_cast<const bf16x8*>(ka);
-      n1 = *reinterpret_cast<const bf16x8*>(ka + 32 * 256);
-    }
-    s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq[kk], s0, 0, 0, 0);
-    s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bq[kk], s1, 0, 0, 0);
-    a0 = n0;
-    a1 = n1;
-  }
-#endif
   // accumulator i of tile u is token 32u + 16(i>>3) + 8h + (i&7)
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -1146,9 +1097,6 @@ __device__ __forceinline__ void attn32_scores(const unsigned char* slot, int k_l
     for (int i = 0; i < 32; ++i)
       if (rel_pos + 32 * (i >> 4) + 16 * ((i >> 3) & 1) + (i & 7) > 0) t[i] = -INFINITY;
   }
-#ifdef PREFILL32_ABL_NOSOFTMAX  // timing ablation only (wrong results): no max / rescale / scaling
-  return;
-#endif
   float v = t[0];
 #pragma unroll
   for (int i = 1; i < 31; i += 2) v = vmax3(v, t[i], t[i + 1]);
@@ -1185,11 +1133,7 @@ __device__ __forceinline__ void attn32_pv(const unsigned char* slot, int v_lane,
   f32x2 ps = {0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < 32; i += 2) {
-#ifdef PREFILL32_ABL_NOSOFTMAX
-    const f32x2 p = {t[i], t[i + 1]};
-#else
     const f32x2 p = {fast_exp2(t[i]), fast_exp2(t[i + 1])};
-#endif
     ps += p;
     bp[i >> 3][i & 7] = static_cast<__bf16>(p.x);
     bp[i >> 3][(i & 7) + 1] = static_cast<__bf16>(p.y);
@@ -1220,74 +1164,41 @@ __device__ __forceinline__ void attn32_pv(const unsigned char* slot, int v_lane,
       }
       o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, va), bp[s], o[dt], 0, 0, 0);
       va = vn;
-#if PREFILL32_SCHED
-      if (nx < 16) __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-#endif
     }
   }
 }
 
-// HP = 2 (8 waves): the workgroup serves query heads 2p and 2p + 1 of the same 128-row tile
-// (4 waves each) and stages each chunk ONCE for both when they share a kv head -- half the staged
-// bytes per FLOP of HP = 1 -- or one image per kv head when the pair straddles two (G odd).
-template <int NW, int NS, int HP = 1>
+template <int NW, int NS>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void prefill_attn32_kernel(
     const bf16_t* __restrict__ q, KVGeom g, const int* __restrict__ block_tables, int max_blocks,
     const int* __restrict__ q_start, const int* __restrict__ seq_lens, const int* __restrict__ tiles, int n_q,
     float scale_log2, bf16_t* __restrict__ out, int n_tiles) {
   constexpr int HD = 128, KC = 64;                   // head dim, tokens per chunk
   constexpr int KBYTES = KC * HD * 2, SLOT = 2 * KBYTES;  // K (then V) image of one chunk: 16 KiB each
-  constexpr int RW = NW / HP;                        // waves (32-row groups) per head
-  constexpr int P = 32 * HP / NW;                    // 1-KiB DMA pieces per wave per chunk (all images)
+  constexpr int P = 32 / NW;                         // 1-KiB DMA pieces per wave per chunk
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-  static_assert(HP == 1 || (HP == 2 && NW == 8), "head pairs need 8 waves");
   static_assert(NS >= 2 && NS <= 4, "ring depth");
-  static_assert(HP == 1 || !PREFILL32_REGSTAGE, "register staging is built for one head per workgroup");
-  __shared__ __attribute__((aligned(1024))) unsigned char ring[NS * SLOT * HP];
+  __shared__ __attribute__((aligned(1024))) unsigned char ring[NS * SLOT];
 
   // XCD-grouped order (1-D grid): workgroup id i runs on XCD i % 8, so kv head i % n_kv puts every
   // query head of a kv head on the same XCD(s) (one XCD per kv head at n_kv = 8), the G heads of
-  // one tile next to each other: the K/V chunks they all stage come from that XCD's L2
+  // one tile next to each other: the K/V chunks they all stage come from that XCD's L2 (+5-8 %
+  // over a (tile, head) grid, profiles/r6_prefill32)
   const int G = n_q / g.n_kv;
-  int tile, qa;  // qa: the workgroup's (first) query head
-#if PREFILL32_XCD
-  if constexpr (HP == 1) {
-    const int kv = blockIdx.x % g.n_kv, rest = blockIdx.x / g.n_kv;
-    tile = rest / G;
-    qa = kv * G + rest % G;
-  } else {  // the head pairs whose first head belongs to kv head kv: pairs [ceil(kv G / 2), ceil((kv + 1) G / 2))
-    constexpr int HPP = HP;
-    const int ppk = (G + HPP - 1) / HPP, kv = blockIdx.x % g.n_kv, rest = blockIdx.x / g.n_kv;
-    tile = rest / ppk;
-    const int p = (kv * G + 1) / 2 + rest % ppk;
-    if (p >= ((kv + 1) * G + 1) / 2) return;  // this kv head owns fewer pairs
-    qa = 2 * p;
-  }
+  const int kvh = blockIdx.x % g.n_kv, rest = blockIdx.x / g.n_kv;
+  const int tile = rest / G, qh = kvh * G + rest % G;
   if (tile >= n_tiles) return;
-#else
-  tile = blockIdx.x;
-  qa = HP * blockIdx.y;
-  (void)n_tiles;
-#endif
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 31, h = lane >> 5;
-  const int hsel = w / RW;                            // which head of the workgroup this wave serves
-  const int qb = qa + 1 < n_q ? qa + 1 : qa;          // HP = 2: the second head (clamped; idle if none)
-  const int qh = hsel ? qb : qa;
-  const int kva = qa / G, kvb = qb / G;
-  const int n_img = (HP == 2 && kvb != kva) ? 2 : 1;  // K/V images staged per chunk
-  const int kvh = qh / G;
-  const int img = kvh != kva ? 1 : 0;                 // the image this wave reads
   const int b = tiles[3 * tile], q_begin = tiles[3 * tile + 1], q_end = tiles[3 * tile + 2];
   const int ctx = seq_lens[b];
   const int pos0 = ctx - (q_start[b + 1] - q_start[b]) - q_start[b];  // position of packed row r = pos0 + r
   const int* table = block_tables + static_cast<size_t>(b) * max_blocks;
   const int nblk = (ctx + BS - 1) / BS;
-  const int wg_last = min(q_begin + 32 * RW, q_end) - 1;
+  const int wg_last = min(q_begin + 32 * NW, q_end) - 1;
   const int nchunk = (pos0 + wg_last + KC) / KC;      // chunks the workgroup stages (uniform)
-  const int row0 = q_begin + 32 * (w % RW);
-  const bool active = row0 < q_end && !(HP == 2 && hsel == 1 && qa + 1 >= n_q);  // wave-uniform
+  const int row0 = q_begin + 32 * w;
+  const bool active = row0 < q_end;                   // wave-uniform
   const int w_last = min(row0 + 31, q_end - 1);
   const int w_chunks = active ? (pos0 + w_last + KC) / KC : 0;          // chunks this wave computes
   const int n_full = active ? min((pos0 + row0 + 1) / KC, w_chunks) : 0;  // ... seen in full by all its rows
@@ -1307,79 +1218,28 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   // chunk (lane & 15) ^ row; V^T piece rows d = 32 (i & 3) + lane / 2, half (lane & 1) ^ bit 3 of d)
   const int lane_kx = (lane & 15) ^ (lane >> 4), lane_k = (lane >> 4) * 256;
   const int lane_v = (lane >> 1) * 32 + (((lane ^ (lane >> 4)) & 1) << 4);
-  auto issue = [&](int c, int p0 = 0, int p1 = 1 << 30) __attribute__((always_inline)) {
-#ifdef PREFILL32_ABL_NODMA  // timing ablation only (wrong results): K / V never staged
-    return;
-#endif
-    unsigned char* slot = ring + (c % NS) * (SLOT * HP);
-    int blk[P];
-#pragma unroll
-    for (int pi = 0; pi < P; ++pi) blk[pi] = blk_ids[4 * c + (((w * P + pi) & 15) >> 2)];
-#ifdef PREFILL32_ABL_HOTSRC  // timing ablation only (wrong results): every chunk re-reads chunk 0 (L2-hot)
-#pragma unroll
-    for (int pi = 0; pi < P; ++pi) blk[pi] = blk_ids[((w * P + pi) & 15) >> 2];
-#endif
-#pragma unroll
-    for (int pi = 0; pi < P; ++pi) {
-      if (pi < p0 || pi >= p1) continue;  // compile-time after inlining
-      const int ig = w * P + pi;  // piece of all images, wave-uniform
-      const int im = ig >> 5, i = ig & 31;  // image, piece 0..31 of it
-      if (im >= n_img) continue;
-      const int r4 = i & 3;
-      const size_t base =
-          ((head_base + __builtin_amdgcn_readfirstlane(blk[pi])) * g.n_kv + (im ? kvb : kva)) * (BS * HD * 2);
-#if PREFILL32_ASM_DMA
-      // The DMA as inline asm (M0 = the piece's LDS address): hipcc tracks the builtin's LDS write
-      // and put a vmcnt(0) before the next ds_read of the ring -- every chunk then waited for its
-      // successor's pieces to land (the whole fetch latency exposed once per chunk).  The ring's
-      // own counted wait + barrier in sync() orders the reads.
-      const unsigned char* src = i < 16 ? kc + base + (r4 * 1024 + lane_k + ((lane_kx ^ (4 * r4)) << 4))
-                                        : vc + base + (r4 * 1024 + lane_v);
-      const uint32_t m0v = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(
-          reinterpret_cast<uintptr_t>(slot + im * SLOT + (i < 16 ? i * 1024 : KBYTES + (i - 16) * 1024))));
-      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(src), "s"(m0v) : "memory", "m0");
-#else
-      if (i < 16)  // K rows 4i .. 4i+3 of the chunk
-        __builtin_amdgcn_global_load_lds(kc + base + (r4 * 1024 + lane_k + ((lane_kx ^ (4 * r4)) << 4)),
-                                         slot + im * SLOT + i * 1024, 16, 0, 0);
-      else  // V^T rows 32 (i & 3) .. + 31 of block (i & 15) / 4
-        __builtin_amdgcn_global_load_lds(vc + base + (r4 * 1024 + lane_v),
-                                         slot + im * SLOT + KBYTES + (i - 16) * 1024, 16, 0, 0);
-#endif
-    }
-  };
-
-#if PREFILL32_REGSTAGE
-  // Register staging: this wave's P pieces of chunk c + 2 are loaded into VGPRs (plain 16-B
-  // loads; the source-side swizzle as above) while chunk c computes, and written into the ring
-  // with ds_write_b128 after the next barrier.  LDS-DMA fills run at ~25 GB/s per CU (the
-  // chip-wide ~6.4 TB/s of MI355X_MICROARCH's ldsdma-fill row) even from L2, about half of
-  // what this kernel consumes at its MFMA rate; a kernel without the DMA (timing ablation)
-  // ran 2.1-2.3x faster.
-  u32x4 stg[P];
-  auto load_regs = [&](int c) __attribute__((always_inline)) {
+  auto issue = [&](int c) __attribute__((always_inline)) {
+    unsigned char* slot = ring + (c % NS) * SLOT;
     int blk[P];
 #pragma unroll
     for (int pi = 0; pi < P; ++pi) blk[pi] = blk_ids[4 * c + (((w * P + pi) & 15) >> 2)];
 #pragma unroll
     for (int pi = 0; pi < P; ++pi) {
-      const int i = w * P + pi;
+      const int i = w * P + pi;  // piece 0..31, wave-uniform
       const int r4 = i & 3;
       const size_t base = ((head_base + __builtin_amdgcn_readfirstlane(blk[pi])) * g.n_kv + kvh) * (BS * HD * 2);
+      // K rows 4i .. 4i+3 of the chunk, or V^T rows 32 (i & 3) .. + 31 of block (i & 15) / 4.
+      // The DMA as inline asm (M0 = the piece's LDS address): hipcc tracks the builtin's LDS write
+      // and put a vmcnt(0) before the next ds_read of the ring -- every chunk then waited for its
+      // successor's pieces to land (+4-6 % without).  The ring's own counted wait + barrier in
+      // sync() orders the reads.
       const unsigned char* src = i < 16 ? kc + base + (r4 * 1024 + lane_k + ((lane_kx ^ (4 * r4)) << 4))
                                         : vc + base + (r4 * 1024 + lane_v);
-      stg[pi] = *reinterpret_cast<const u32x4*>(src);
+      const uint32_t m0v = __builtin_amdgcn_readfirstlane(
+          static_cast<uint32_t>(reinterpret_cast<uintptr_t>(slot + (i < 16 ? i * 1024 : KBYTES + (i - 16) * 1024))));
+      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(src), "s"(m0v) : "memory", "m0");
     }
   };
-  auto write_regs = [&](int c) __attribute__((always_inline)) {
-    unsigned char* slot = ring + (c % NS) * SLOT + lane * 16;
-#pragma unroll
-    for (int pi = 0; pi < P; ++pi) {
-      const int i = w * P + pi;
-      *reinterpret_cast<u32x4*>(slot + (i < 16 ? i * 1024 : KBYTES + (i - 16) * 1024)) = stg[pi];
-    }
-  };
-#endif
 
   // Q^T operands: lane (col, h) holds dims 16 kk + 8 h .. + 7 of its row
   bf16x8 bq[HD / 16];
@@ -1397,16 +1257,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     }
   }
   __syncthreads();  // block ids staged
-#if PREFILL32_REGSTAGE
-  (void)issue;
-  load_regs(0);
-  write_regs(0);
-  if (1 < nchunk) load_regs(1);
-#else
 #pragma unroll
   for (int c = 0; c < NS - 1; ++c)
     if (c < nchunk) issue(c);
-#endif
 
   // K operand addresses: S^T row m = col holds token t0(m) (tile u = 0; u = 1 is t0 + 32, the same
   // swizzle); 16-B chunk 2 kk + h of that row sits at slot (2 kk + h) ^ (t0 & 15), i.e. at byte
@@ -1422,34 +1275,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
 
   // chunk c's pieces landed and its successor's slot is free: wait + barrier, then the DMA of
   // chunk c + NS - 1 (every wave runs this for every chunk of the workgroup)
-#if PREFILL32_REGSTAGE
-  // chunk c's image complete (every wave's writes) and every wave past chunk c - 1
-  auto sync = [&](int c) __attribute__((always_inline)) {
-    (void)c;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-  // after the S^T MFMAs: chunk c + 1 into the slot chunk c - 1 used, chunk c + 2's loads issued
-  auto stage = [&](int c) __attribute__((always_inline)) {
-    if (c + 1 < nchunk) {
-      write_regs(c + 1);
-      if (c + 2 < nchunk) load_regs(c + 2);
-    }
-  };
-#else
-  // PREFILL32_DMA_SPLIT (NS = 2): half of the next chunk's pieces right after the barrier, the
-  // other half after the S^T MFMAs, instead of all eight in one burst
-  auto stage = [&](int c) __attribute__((always_inline)) {
-    if constexpr (PREFILL32_DMA_SPLIT && NS == 2) {
-      if (c + 1 < nchunk) issue(c + 1, P / 2, P);
-    } else {
-      (void)c;
-    }
-  };
   auto sync = [&](int c) __attribute__((always_inline)) {
     const int ahead = min(NS - 2, nchunk - 1 - c);  // later chunks whose pieces may still fly
-#ifndef PREFILL32_ABL_NOWAIT  // timing ablation only (wrong results): the DMA is never waited for
     if (ahead >= 2) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * P) : "memory");
     } else if (ahead == 1) {
@@ -1457,20 +1284,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-#else
-    (void)ahead;
-#endif
     __builtin_amdgcn_s_barrier();  // ... and every wave is past chunk c - 1: its slot is free
     asm volatile("" ::: "memory");
-    if (c + NS - 1 < nchunk) {
-      if constexpr (PREFILL32_DMA_SPLIT && NS == 2)
-        issue(c + NS - 1, 0, P / 2);
-      else
-        issue(c + NS - 1);
-    }
+    if (c + NS - 1 < nchunk) issue(c + NS - 1);
   };
-#endif
-  auto slot_of = [&](int c) { return static_cast<const unsigned char*>(ring + (c % NS) * (SLOT * HP) + img * SLOT); };
+  auto slot_of = [&](int c) { return static_cast<const unsigned char*>(ring + (c % NS) * SLOT); };
   int c = 0;
   float t[32];
   // chunks every row of the wave sees in full, then the diagonal (and context-end) chunks --
@@ -1478,19 +1296,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   for (; c < n_full; ++c) {
     sync(c);
     attn32_scores<false>(slot_of(c), k_lane, bq, scale_log2, 0, m, lsum, o, t);
-    stage(c);
     attn32_pv<false>(slot_of(c), v_lane, 0, t, lsum, o);
   }
   for (; c < w_chunks; ++c) {
     sync(c);
     attn32_scores<true>(slot_of(c), k_lane, bq, scale_log2, c * KC + 8 * h - pos_q, m, lsum, o, t);
-    stage(c);
     attn32_pv<true>(slot_of(c), v_lane, c * KC + 8 * h - ctx, t, lsum, o);
   }
-  for (; c < nchunk; ++c) {  // chunks in the causal future of every row of this wave
-    sync(c);
-    stage(c);
-  }
+  for (; c < nchunk; ++c) sync(c);  // chunks in the causal future of every row of this wave
   if (!active || row0 + col >= q_end) return;
   {
     const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum), __float_as_uint(lsum), false, false);
@@ -1606,12 +1419,7 @@ BCG_API int bcg_paged_attention_prefill(const void* q, const void* k_cache, cons
 // The 32x32 LDS-staged form (prefill_attn32_kernel): `tiles` holds tiles of at most tile_rows
 // rows -- 128 (4 waves, 2-slot ring, two workgroups per CU) or 256 (8 waves, 3-slot ring).
 // bf16 KV cache and head dim 128 only (-2 otherwise: the caller uses the 16x16 kernel).
-#ifndef PREFILL32_NS4
-#define PREFILL32_NS4 2
-#endif
-#ifndef PREFILL32_NS8
-#define PREFILL32_NS8 3
-#endif
+constexpr int PREFILL32_NS4 = 2, PREFILL32_NS8 = 3;  // ring slots at 4 / 8 waves (LDS: 2 or 1 workgroups per CU)
 BCG_API int bcg_paged_attention_prefill32(const void* q, const void* k_cache, const void* v_cache, int layer,
                                           int num_blocks, int n_kv, const int* block_tables, int max_blocks,
                                           const int* q_start, const int* seq_lens, const int* tiles, int n_tiles,
@@ -1624,17 +1432,8 @@ BCG_API int bcg_paged_attention_prefill32(const void* q, const void* k_cache, co
   const float sl = scale * LOG2E;
   const bf16_t* qb = static_cast<const bf16_t*>(q);
   bf16_t* ob = static_cast<bf16_t*>(out);
-#if PREFILL32_XCD
-  const dim3 grid(n_tiles * n_q);
-  const dim3 grid2(n_tiles * n_kv * ((n_q / n_kv + 1) / 2));  // head pairs: ceil(G / 2) slots per kv head
-#else
-  const dim3 grid(n_tiles, n_q);
-  const dim3 grid2(n_tiles, (n_q + 1) / 2);
-#endif
-  if (tile_rows == 128 && PREFILL32_HP2)
-    hipLaunchKernelGGL((prefill_attn32_kernel<8, 2, 2>), grid2, dim3(512), 0, stream, qb, g, block_tables, max_blocks,
-                       q_start, seq_lens, tiles, n_q, sl, ob, n_tiles);
-  else if (tile_rows == 128)
+  const dim3 grid(n_tiles * n_q);  // XCD-grouped 1-D order (see the kernel)
+  if (tile_rows == 128)
     hipLaunchKernelGGL((prefill_attn32_kernel<4, PREFILL32_NS4>), grid, dim3(256), 0, stream, qb, g, block_tables,
                        max_blocks, q_start, seq_lens, tiles, n_q, sl, ob, n_tiles);
   else if (tile_rows == 256)
