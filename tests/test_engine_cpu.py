@@ -304,3 +304,40 @@ def test_finished_rows_skip_attention_same_outputs(fresh_engine_state, monkeypat
         outs[skip] = [o.outputs[0].text for o in llm.generate(prompts, params)]
         llm.shutdown()
     assert outs["1"] == outs["0"]
+
+
+def test_prefill_tile_table_covers_rows(fresh_engine_state, monkeypatch):
+    """The prefill tile table the engine builds for the HIP kernels (ops.prefill_tile_rows rows per
+    tile: 128 selects the 32x32 LDS kernel): every packed query row of a chunk in exactly one tile
+    of its own sequence, no tile longer than tile_rows, deepest tiles first -- checked on the torch
+    backend by recording what reaches paged_attention_prefill."""
+    from byzantine_consensus_llm_agents_amd.engine import LLM, SamplingParams
+    from byzantine_consensus_llm_agents_amd.ops import get_ops
+    ops = get_ops("torch")
+    seen = []
+    orig = ops.paged_attention_prefill
+
+    def record(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale, max_q_len=None, tiles=None,
+               tile_rows=64):
+        if layer == 0:
+            seen.append((tiles.cpu().tolist(), tile_rows, q_start.cpu().tolist(), seq_lens.cpu().tolist()))
+        return orig(q, k_cache, v_cache, layer, block_tables, q_start, seq_lens, scale, max_q_len, tiles, tile_rows)
+
+    monkeypatch.setattr(ops, "paged_attention_prefill", record)
+    monkeypatch.setattr(ops, "prefill_tile_rows", lambda hd, kv_fp8=False, max_blocks=0: 128)
+    llm = LLM("bcg/tiny-qwen3", backend="torch", seed=2, max_model_len=1024, kv_cache_gb=0.05,
+              max_batch_seqs=8, prefill_chunk_tokens=256, prefix_caching=False)
+    prompts = [f"<|im_start|>user\nagent_{i} " + "history " * (30 * i + 7) + "<|im_end|>\n" for i in range(5)]
+    llm.generate(prompts, [SamplingParams(temperature=0.0, max_tokens=2)] * 5)
+    llm.shutdown()
+    assert seen
+    for tiles, rows, q_start, seq_lens in seen:
+        assert rows == 128
+        covered = [0] * q_start[-1]
+        for b, t0, t1 in tiles:
+            assert q_start[b] <= t0 < t1 <= q_start[b + 1] and t1 - t0 <= rows
+            for r in range(t0, t1):
+                covered[r] += 1
+        assert covered == [1] * q_start[-1]
+        depth = [seq_lens[b] - (q_start[b + 1] - t0) for b, t0, _ in tiles]  # keys before the tile
+        assert depth == sorted(depth, reverse=True)
